@@ -1,0 +1,185 @@
+/*
+ * llmi.h -- C ABI of the MI355X-native Llama-2 decode engine (libllmi.so).
+ *
+ * This is the drop-in boundary for the reference's decode hot path
+ * (Mr-wang27/llm-inference, the src/kernels launcher headers + the Llama<T> decode
+ * loop). Every entry point is plain C: device pointers, sizes, dtype enums,
+ * an opaque hipStream_t. No torch or C++ types cross it. Each function cites
+ * the reference interface it replaces (paths relative to the reference root).
+ *
+ * Conventions
+ *  - return 0 (LLMI_OK) on success, negative on error; never throws.
+ *    LLMI_EINVAL = bad argument, LLMI_EUNSUPPORTED = valid but not built,
+ *    LLMI_EHIP - hipError_t = HIP runtime error. llmi_last_error() returns a
+ *    thread-local message "[llmi][ERROR] ..." (the reference's LLM_CHECK text
+ *    convention, src/utils/macro.h:113-133).
+ *  - Row-major tensors. Linear weights are [out_features, in_features]
+ *    (PyTorch nn.Linear layout; the reference calls cuBLAS with trans_b on
+ *    exactly this layout, src/kernels/linear.cu:38-99).
+ *  - Activations are fp32 unless a dtype argument says otherwise; weights
+ *    may be fp32, fp16 or int8 (+ per-row fp16 scales, W8A16).
+ *  - Nothing here blocks the host or allocates, except engine create/destroy and
+ *    the engine's host<->device copy helpers; all launches are stream-ordered
+ *    and graph-capturable.
+ */
+#ifndef LLMI_H_
+#define LLMI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* llmi_stream_t; /* hipStream_t; NULL = legacy default stream */
+
+enum llmi_dtype { LLMI_F32 = 0, LLMI_F16 = 1, LLMI_I8 = 2, LLMI_I32 = 3 };
+
+#define LLMI_OK 0
+#define LLMI_EINVAL (-1)
+#define LLMI_EUNSUPPORTED (-2)
+#define LLMI_ENOMEM (-3)
+#define LLMI_EHIP (-1000)
+
+const char* llmi_last_error(void);
+const char* llmi_version(void);
+
+/* ======================================================================
+ * Operator API: one entry per reference launcher on the decode path.
+ * ==================================================================== */
+
+/* launchInputEmbedding (src/kernels/input_embedding.h:6-9):
+ * out[t, :] = table[ids[t], :] for t < n_tokens; out fp32 [n_tokens, hidden].
+ * Bit-exact copy (fp16 -> fp32 widening is exact). ids out of range -> error flag. */
+int llmi_embedding(const int32_t* ids, int n_tokens, const void* table, int table_dtype,
+                   int vocab, int hidden, float* out, llmi_stream_t stream);
+
+/* launchRMSNorm (src/kernels/rmsnorm_kernel.h:11-17):
+ * out = gamma * (x * rsqrt(mean(x^2) + eps)) per row (modeling_llama.py:112-117).
+ * residual_out (nullable) receives the pre-norm x (the reference's intent;
+ * its kernel aliases it). x may alias out. */
+int llmi_rmsnorm(const float* x, float* out, float* residual_out, const void* gamma, int gamma_dtype,
+                 int n_tokens, int hidden, float eps, llmi_stream_t stream);
+
+/* launchFusedAddBiasResidualRMSNorm (src/kernels/fused_addresidual_norm.h:9-15):
+ * residual = residual + decoder_out (+ bias); decoder_out = rmsnorm(residual) * gamma.
+ * bias is nullable (Llama-2 has none). */
+int llmi_add_residual_rmsnorm(float* residual, float* decoder_out, const void* bias, int bias_dtype,
+                              const void* gamma, int gamma_dtype, int n_tokens, int hidden, float eps,
+                              llmi_stream_t stream);
+
+/* launchAddResidual (src/kernels/add_residual.h:8-13): decoder_out += residual. */
+int llmi_add_residual(const float* residual, float* decoder_out, int n_tokens, int hidden,
+                      llmi_stream_t stream);
+
+/* launchAct (src/kernels/act_kernel.h:8-9): in [n, 2, inter] (gate then up),
+ * out[n, i] = silu(gate) * up. */
+int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llmi_stream_t stream);
+
+/* launchLinearGemm (src/kernels/linear.h:16-22) with trans_b = true:
+ * y[m, n] = sum_k x[m, k] * W[n, k] (* scales[n] for int8). fp32 accumulate.
+ * decode (m <= 8): HBM-streaming GEMV; m > 8: batched (prefill) path. */
+int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m,
+                int n, int k, llmi_stream_t stream);
+
+/* launchRoPE (src/kernels/qkv_bias_and_RoPE.h:40-42) for one decode token:
+ * rotates q (heads) and k (kv_heads) of the fused qkv row [ (h + 2kv) * d ]
+ * in place at position `pos` (= step - 1), pairs (i, i + d/2),
+ * theta_i = base^(-2i/d) (modeling_llama.py:123-156, 204-236). */
+int llmi_rope_decode(float* qkv, int pos, int heads, int kv_heads, int head_dim, float base,
+                     llmi_stream_t stream);
+
+/* launchDecoderMaskedMHA (src/kernels/fused_decoder_self_attention.h:10-19):
+ * writes k, v of the fused qkv row into the cache slot `pos` of `layer`
+ * (cache [layers, kv_heads, max_seq, head_dim], dtype f16 or f32), then
+ * out[h] = softmax(q_h . K^T / sqrt(d)) V over positions 0..pos (fp32
+ * softmax, split-KV over workgroups with a log-sum-exp merge).
+ * rope != 0 additionally applies RoPE to q/k first (the engine's fused form).
+ * workspace: >= llmi_attn_workspace_bytes(...) bytes of device memory whose
+ * counter region is zero before the first call (it is left zeroed). */
+size_t llmi_attn_workspace_bytes(int heads, int head_dim, int max_seq);
+int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_dtype, int layer,
+                     int max_seq, int pos, int heads, int kv_heads, int head_dim, int rope,
+                     float rope_base, float* out, void* workspace, llmi_stream_t stream);
+
+/* launchTopKforBeamSearch + launchSampling (src/kernels/topK.h:51-56,
+ * sampling.h:12-18) as wired by Llama<T> (K = beamwidth = 1, llama.cpp:59):
+ * greedy argmax over logits[n]; ties -> lowest index. out_id: device int32. */
+int llmi_argmax(const float* logits, int n, int32_t* out_id, llmi_stream_t stream);
+
+/* Synthetic-weight generator (replaces LlamaLayerWeight::loadWeights() dummy
+ * path, src/weights/llama/layer_weights.cc:69-146). Fills the [rows, cols]
+ * slice (row0, col0) of a logical [*, ld] tensor `tid` with llmi-prng-v1
+ * values (spec: oracle/prng.py). kind: 0 linear, 1 embedding, 2 norm gamma
+ * (rows = 1), 3 int8 weight, 4 int8 per-row scale (cols = 1).
+ * out_dtype: F16 or F32 (values identical), I8 for kind 3, F16 for kind 4. */
+enum llmi_synth_kind { LLMI_SYN_LINEAR = 0, LLMI_SYN_EMBED = 1, LLMI_SYN_GAMMA = 2,
+                       LLMI_SYN_INT8 = 3, LLMI_SYN_INT8_SCALE = 4 };
+int llmi_synth_fill(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
+                    int cols, int row0, int col0, int ld, llmi_stream_t stream);
+/* Host (CPU) twin of llmi_synth_fill, for checking the generator without a GPU. */
+int llmi_synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
+                         int cols, int row0, int col0, int ld);
+/* Synthetic prompt ids (bench config: 8 PRNG ids). Host only. */
+int llmi_synth_prompt(uint64_t seed, int n, int vocab, int32_t* out);
+
+/* ======================================================================
+ * Engine API: the Llama<T> decode loop (src/models/llama/llama.cpp:318-349
+ * continueTokenGen, :362-457 Response) with the per-layer sequence of
+ * LlamaSelfDecoder::forward (src/layers/decoder/self_decoder.cpp:23-89).
+ * One engine per GPU (per TP rank). The whole token step -- embedding,
+ * L x {rmsnorm+QKV, rope+kv-write+attention, O+residual, rmsnorm+gate_up+silu,
+ * down+residual}, final norm + lm_head + argmax -- is one hipGraph replay;
+ * positions and token ids live in device memory, so no host sync per token.
+ * ==================================================================== */
+typedef struct llmi_config {
+    int hidden, heads, kv_heads, head_dim, inter, layers, vocab, max_seq;
+    float rms_eps, rope_base;
+    int weight_dtype; /* LLMI_F16 (default), LLMI_F32 (reference Llama<float>), LLMI_I8 (W8A16) */
+    int kv_dtype;     /* LLMI_F16 (throughput) or LLMI_F32 (parity) */
+    int tp_rank, tp_world;
+} llmi_config;
+
+typedef struct llmi_engine llmi_engine;
+
+/* Fill `cfg` with a preset: "llama2-7b", "llama2-13b", "tiny". */
+int llmi_config_preset(const char* name, llmi_config* cfg);
+
+/* RCCL unique id (128 bytes) for tensor parallel: rank 0 creates it, the
+ * launcher broadcasts it (any side channel), every rank passes it to create. */
+int llmi_tp_unique_id(void* out128);
+
+/* device: HIP device ordinal. tp_id: 128-byte RCCL id or NULL when tp_world == 1. */
+int llmi_engine_create(const llmi_config* cfg, int device, const void* tp_id, llmi_engine** out);
+int llmi_engine_destroy(llmi_engine* e);
+/* Llama<T>::loadWeightsFromDummy (src/models/llama/llama.h) with llmi-prng-v1 weights. */
+int llmi_engine_load_synthetic(llmi_engine* e, uint64_t seed);
+/* Reset the sequence and stage a prompt (device copy). */
+int llmi_engine_set_prompt(llmi_engine* e, const int32_t* ids, int n);
+/* Run n forward steps (one token each). use_graph: replay the captured hipGraph. */
+int llmi_engine_decode(llmi_engine* e, int n_steps, int use_graph);
+/* Block until the engine stream is idle. */
+int llmi_engine_sync(llmi_engine* e);
+/* Tokens[0 .. n) of the sequence so far: prompt ids followed by generated ids
+ * (position p's token; the token after the last forward is included). */
+int llmi_engine_tokens(llmi_engine* e, int32_t* out, int n, int* n_valid);
+/* fp32 logits of the last forward (this rank's vocab shard under TP). */
+int llmi_engine_logits(llmi_engine* e, float* out, int n);
+/* fp32 residual stream (hidden) after the last forward. */
+int llmi_engine_hidden(llmi_engine* e, float* out, int n);
+/* Read one cache slot (layer, pos) of K or V as fp32 [kv_heads_local, head_dim]. */
+int llmi_engine_kv_slot(llmi_engine* e, int layer, int pos, int which_v, float* out);
+/* Bytes of weights (and KV per position) one forward streams on this rank. */
+int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes_per_pos);
+/* hipStream_t the engine launches on. */
+llmi_stream_t llmi_engine_stream(llmi_engine* e);
+/* Time `iters` eager launches of one kernel of layer 0 (HIP events on the
+ * engine stream). which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head.
+ * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
+int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLMI_H_ */

@@ -1,0 +1,123 @@
+// extern "C" operator API (include/llmi.h): thin argument checks over the
+// kernels in gemv.hip / attn.hip / ops.hip. Never throws; errors are return
+// codes plus a thread-local message.
+#include <string>
+
+#include "kernels.h"
+#include "prng.h"
+
+namespace llmi {
+namespace {
+thread_local std::string g_last_error;
+}
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace llmi
+
+using namespace llmi;
+
+#define STREAM(s) reinterpret_cast<hipStream_t>(s)
+
+extern "C" {
+
+const char* llmi_last_error(void) { return llmi::g_last_error.c_str(); }
+const char* llmi_version(void) { return "llmi 0.1 (gfx950)"; }
+
+int llmi_embedding(const int32_t* ids, int n_tokens, const void* table, int table_dtype, int vocab, int hidden,
+                   float* out, llmi_stream_t stream) {
+    return embedding_launch(ids, n_tokens, table, table_dtype, vocab, hidden, out, STREAM(stream));
+}
+
+int llmi_rmsnorm(const float* x, float* out, float* residual_out, const void* gamma, int gamma_dtype, int n_tokens,
+                 int hidden, float eps, llmi_stream_t stream) {
+    return rmsnorm_launch(x, out, residual_out, gamma, gamma_dtype, n_tokens, hidden, eps, STREAM(stream));
+}
+
+int llmi_add_residual_rmsnorm(float* residual, float* decoder_out, const void* bias, int bias_dtype,
+                              const void* gamma, int gamma_dtype, int n_tokens, int hidden, float eps,
+                              llmi_stream_t stream) {
+    return add_resid_rmsnorm_launch(residual, decoder_out, bias, bias_dtype, gamma, gamma_dtype, n_tokens, hidden,
+                                    eps, STREAM(stream));
+}
+
+int llmi_add_residual(const float* residual, float* decoder_out, int n_tokens, int hidden, llmi_stream_t stream) {
+    return add_resid_launch(residual, decoder_out, n_tokens, hidden, STREAM(stream));
+}
+
+int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llmi_stream_t stream) {
+    return silu_mul_launch(gate_up, out, n_tokens, inter, STREAM(stream));
+}
+
+int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
+                llmi_stream_t stream) {
+    LLMI_REQUIRE(m >= 1 && n >= 1 && k >= 1, "linear: m, n, k must be >= 1");
+    GemvArgs a;
+    a.w = w;
+    a.w_dtype = w_dtype;
+    a.scales = reinterpret_cast<const __half*>(w_scales);
+    a.n_rows = n;
+    a.k = k;
+    a.epi = EPI_STORE;
+    // TODO(prefill): m > 8 belongs on the MFMA GEMM; rows go through the GEMV meanwhile.
+    for (int i = 0; i < m; ++i) {
+        a.x = x + (size_t)i * k;
+        a.y = y + (size_t)i * n;
+        LLMI_TRY(gemv_launch(a, STREAM(stream)));
+    }
+    return LLMI_OK;
+}
+
+int llmi_rope_decode(float* qkv, int pos, int heads, int kv_heads, int head_dim, float base, llmi_stream_t stream) {
+    return rope_decode_launch(qkv, pos, heads, kv_heads, head_dim, base, STREAM(stream));
+}
+
+size_t llmi_attn_workspace_bytes(int heads, int head_dim, int max_seq) {
+    return attn_workspace_bytes(heads, head_dim, max_seq);
+}
+
+int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_dtype, int layer, int max_seq, int pos,
+                     int heads, int kv_heads, int head_dim, int rope, float rope_base, float* out, void* workspace,
+                     llmi_stream_t stream) {
+    LLMI_REQUIRE(layer >= 0, "attn: layer must be >= 0");
+    AttnArgs a;
+    const size_t off = (size_t)layer * kv_heads * max_seq * head_dim * dtype_size(cache_dtype);
+    a.qkv = qkv;
+    a.k_cache = (char*)k_cache + off;
+    a.v_cache = (char*)v_cache + off;
+    a.cache_dtype = cache_dtype;
+    a.max_seq = max_seq;
+    a.pos_host = pos;
+    a.heads = heads;
+    a.kv_heads = kv_heads;
+    a.head_dim = head_dim;
+    a.rope = rope;
+    a.rope_base = rope_base;
+    a.out = out;
+    a.workspace = workspace;
+    return attn_decode_launch(a, STREAM(stream));
+}
+
+int llmi_argmax(const float* logits, int n, int32_t* out_id, llmi_stream_t stream) {
+    // 256 x 8 B of scratch for the partial keys: a per-process device buffer
+    static unsigned long long* scratch = nullptr;
+    if (!scratch) LLMI_HIP(hipMalloc(&scratch, 256 * sizeof(unsigned long long)));
+    return argmax_launch(logits, n, out_id, scratch, STREAM(stream));
+}
+
+int llmi_synth_fill(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows, int cols, int row0,
+                    int col0, int ld, llmi_stream_t stream) {
+    return synth_fill_launch(out, out_dtype, kind, seed, tid, rows, cols, row0, col0, ld, STREAM(stream));
+}
+
+int llmi_synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows, int cols,
+                         int row0, int col0, int ld) {
+    return synth_fill_host(out, out_dtype, kind, seed, tid, rows, cols, row0, col0, ld);
+}
+
+int llmi_synth_prompt(uint64_t seed, int n, int vocab, int32_t* out) {
+    LLMI_REQUIRE(out && n >= 0 && vocab > 0, "synth_prompt: bad arguments");
+    const uint64_t key = prng::tensor_key(seed, prng::PROMPT);
+    for (int i = 0; i < n; ++i) out[i] = (int32_t)(prng::bits(key, (uint64_t)i) % (uint64_t)vocab);
+    return LLMI_OK;
+}
+
+}  // extern "C"

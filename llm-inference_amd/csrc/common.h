@@ -1,0 +1,110 @@
+// Shared helpers for the llmi HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <stdexcept>
+
+#include "../../include/llmi.h"
+
+namespace llmi {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- errors
+void set_last_error(const std::string& msg);
+
+struct Status {
+    int code = LLMI_OK;
+};
+
+#define LLMI_HIP(expr)                                                                 \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            ::llmi::set_last_error(std::string(#expr) + ": " + hipGetErrorString(_e) + \
+                                   " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+            return LLMI_EHIP - (int)_e;                                                \
+        }                                                                              \
+    } while (0)
+
+#define LLMI_REQUIRE(cond, msg)                                                        \
+    do {                                                                               \
+        if (!(cond)) {                                                                 \
+            ::llmi::set_last_error(std::string("[llmi][ERROR] ") + (msg) + " (" #cond ")"); \
+            return LLMI_EINVAL;                                                        \
+        }                                                                              \
+    } while (0)
+
+#define LLMI_TRY(expr)                  \
+    do {                                \
+        int _rc = (expr);               \
+        if (_rc != LLMI_OK) return _rc; \
+    } while (0)
+
+inline size_t dtype_size(int dt) {
+    switch (dt) {
+        case LLMI_F32: return 4;
+        case LLMI_F16: return 2;
+        case LLMI_I8: return 1;
+        case LLMI_I32: return 4;
+        default: return 0;
+    }
+}
+
+// ------------------------------------------------------------ device math
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(__half v) { return __half2float(v); }
+__device__ __forceinline__ float to_f32(int8_t v) { return (float)v; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `red` needs >= 16 floats of LDS.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += red[i];
+    return t;
+}
+
+// Order-preserving 64-bit key for (value, index) argmax: larger value wins,
+// ties go to the lower index (torch/numpy argmax semantics).
+__host__ __device__ __forceinline__ unsigned long long argmax_key(float v, uint32_t idx) {
+    uint32_t b;
+#ifdef __HIP_DEVICE_COMPILE__
+    b = __float_as_uint(v);
+#else
+    std::memcpy(&b, &v, 4);
+#endif
+    b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    return ((unsigned long long)b << 32) | (unsigned long long)(0xFFFFFFFFu - idx);
+}
+__host__ __device__ __forceinline__ uint32_t argmax_key_index(unsigned long long k) {
+    return 0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull);
+}
+
+// Nontemporal 16-byte weight load: weights are streamed once per token and
+// never fit the 256 MiB Infinity Cache (MI355X_MICROARCH.md, row nt-weights).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt16(const void* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+}  // namespace llmi

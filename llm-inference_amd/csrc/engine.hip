@@ -1,0 +1,628 @@
+// DecodeEngine: the Llama<T> single-stream greedy decode loop on one GPU (or
+// one tensor-parallel rank), as one hipGraph per token.
+//
+// Reference call stack replaced:
+//   Llama<T>::Response / continueTokenGen       src/models/llama/llama.cpp:318-349, 362-457
+//   LlamaSelfDecoder<T>::forward                src/layers/decoder/self_decoder.cpp:23-89
+//   LLaMASelfAttentionLayer<T>::Forward         src/layers/attention/masked_self_attention.cpp:54-92
+//   LLaMAFFNLayer<T>::forward                   src/layers/ffn/ffn.cpp:52-93
+//   LMHeadAndTopKSample                         src/models/llama/llama.cpp:214-269
+// The reference issues ~326 launches per token, each followed by
+// cudaDeviceSynchronize, plus a D2H and an H2D copy per token. Here one token is
+//   step_start (token pick + embedding)
+//   L x [ rmsnorm+QKV gemv | rope+kv-write+split-KV attention | O gemv+residual
+//         (| allreduce) | rmsnorm+gate_up gemv+silu*mul | down gemv+residual (| allreduce) ]
+//   final rmsnorm + lm_head gemv + argmax partials (| allreduce max)
+// = 5L + 2 kernels, captured once into a hipGraph; positions, token ids and the
+// argmax hand-off live in device memory, so tokens are produced with no host sync.
+//
+// HBM layout (one allocation each): all weights contiguous per layer in
+// forward order (qkv, o, gate_up, down, norms), then lm_head, final norm,
+// embedding; KV cache [layers, kv_heads, max_seq, head_dim] per K and V
+// (concat_past_kv.cu:122 layout, batch 1); fp32 activations (16-44 KB) and
+// the decode state in a small scratch block.
+//
+// Tensor parallel: Megatron column/row split over tp_world
+// ranks, one process per GPU; q/k/v and gate/up rows split by heads / inter
+// columns, o and down split on their input columns. Rank 0 adds the residual
+// in the o/down epilogue, every other rank stores its bare partial, and an RCCL
+// all-reduce(sum) over xGMI yields residual + sum of partials in place: 2 per
+// layer. The vocab-parallel lm_head produces per-workgroup argmax keys with
+// global row ids; an all-reduce(max) of the keys gives every rank the same
+// next token. Weights are generated shard-by-shard from the same global PRNG
+// indices, so every TP degree computes the same model.
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "kernels.h"
+#include "prng.h"
+
+namespace llmi {
+
+namespace {
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+}  // namespace
+
+struct Engine {
+    llmi_config c{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // local (per-rank) dims
+    int hl = 0, kvl = 0, ql = 0, kvrows = 0, il = 0, vl = 0;
+    int wdt = LLMI_F16;      // linear weight dtype
+    int edt = LLMI_F16;      // embedding / lm_head / norm dtype
+    size_t wsz = 2, esz = 2;
+
+    struct Layer {
+        void *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
+        __half *qkv_s = nullptr, *o_s = nullptr, *gu_s = nullptr, *down_s = nullptr;
+        void *attn_norm = nullptr, *ffn_norm = nullptr;
+    };
+    std::vector<Layer> layers;
+    void *embed = nullptr, *lm_head = nullptr, *final_norm = nullptr;
+    char* wblob = nullptr;
+    size_t wbytes = 0;
+    uint64_t stream_bytes = 0;  // weight bytes one forward reads
+
+    void *kcache = nullptr, *vcache = nullptr;
+    size_t kv_layer_elems = 0;
+
+    char* scratch = nullptr;
+    float *x = nullptr, *qkv_buf = nullptr, *attn_out = nullptr, *act = nullptr, *logits = nullptr;
+    unsigned long long* partials = nullptr;
+    int lm_grid = 0;
+    void* attn_ws = nullptr;
+    DecodeState* st = nullptr;
+    int32_t *prompt = nullptr, *tokens = nullptr;
+
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    ncclComm_t comm = nullptr;
+    int host_next_pos = 0, prompt_len = 0;
+    uint64_t seed = 0;
+
+    ~Engine() {  // teardown errors are not actionable; ignore them explicitly
+        if (exec) (void)hipGraphExecDestroy(exec);
+        if (graph) (void)hipGraphDestroy(graph);
+        if (comm) (void)ncclCommDestroy(comm);
+        if (wblob) (void)hipFree(wblob);
+        if (kcache) (void)hipFree(kcache);
+        if (vcache) (void)hipFree(vcache);
+        if (scratch) (void)hipFree(scratch);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    // ---------------------------------------------------------------- setup
+    int init(const llmi_config& cfg, int dev, const void* tp_id) {
+        c = cfg;
+        device = dev;
+        const int W = c.tp_world;
+        LLMI_REQUIRE(W >= 1 && c.tp_rank >= 0 && c.tp_rank < W, "engine: bad tp rank/world");
+        LLMI_REQUIRE(c.head_dim == 128, "engine: head_dim must be 128");
+        LLMI_REQUIRE(c.heads * c.head_dim == c.hidden, "engine: hidden != heads * head_dim");
+        LLMI_REQUIRE(c.heads % c.kv_heads == 0, "engine: heads % kv_heads != 0");
+        LLMI_REQUIRE(c.heads % W == 0 && c.kv_heads % W == 0 && c.inter % W == 0 && c.vocab % W == 0,
+                     "engine: heads, kv_heads, inter and vocab must divide by tp_world");
+        LLMI_REQUIRE(c.max_seq > 0 && c.layers > 0 && c.vocab > 0, "engine: bad dims");
+        LLMI_REQUIRE(c.kv_dtype == LLMI_F16 || c.kv_dtype == LLMI_F32, "engine: kv dtype must be f16/f32");
+        wdt = c.weight_dtype;
+        LLMI_REQUIRE(wdt == LLMI_F16 || wdt == LLMI_F32 || wdt == LLMI_I8, "engine: bad weight dtype");
+        edt = (wdt == LLMI_F32) ? LLMI_F32 : LLMI_F16;
+        wsz = dtype_size(wdt);
+        esz = dtype_size(edt);
+        hl = c.heads / W;
+        kvl = c.kv_heads / W;
+        ql = hl * c.head_dim;
+        kvrows = kvl * c.head_dim;
+        il = c.inter / W;
+        vl = c.vocab / W;
+        const int epl = 16 / (int)wsz;
+        LLMI_REQUIRE(c.hidden % epl == 0 && ql % epl == 0 && il % epl == 0,
+                     "engine: hidden, q rows per rank and inter per rank must be multiples of 16 bytes");
+
+        LLMI_HIP(hipSetDevice(device));
+        LLMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        if (W > 1) {
+            LLMI_REQUIRE(tp_id != nullptr, "engine: tp_world > 1 needs the RCCL unique id");
+            ncclUniqueId id;
+            std::memcpy(&id, tp_id, sizeof(id));
+            ncclResult_t r = ncclCommInitRank(&comm, W, id, c.tp_rank);
+            LLMI_REQUIRE(r == ncclSuccess, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+        LLMI_TRY(alloc_weights());
+        LLMI_TRY(alloc_state());
+        return LLMI_OK;
+    }
+
+    int alloc_weights() {
+        const size_t H = c.hidden, A = 256;
+        size_t off = 0;
+        auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, A); return o; };
+        struct Off { size_t qkv, o, gu, down, qs, os, gs, ds, an, fn; };
+        std::vector<Off> lo(c.layers);
+        const size_t qkv_rows = ql + 2 * kvrows;
+        for (int l = 0; l < c.layers; ++l) {
+            Off& t = lo[l];
+            t.qkv = take(qkv_rows * H * wsz);
+            t.o = take(H * ql * wsz);
+            t.gu = take(2 * il * H * wsz);
+            t.down = take(H * il * wsz);
+            if (wdt == LLMI_I8) {
+                t.qs = take(qkv_rows * 2);
+                t.os = take(H * 2);
+                t.gs = take(2 * il * 2);
+                t.ds = take(H * 2);
+            }
+            t.an = take(H * esz);
+            t.fn = take(H * esz);
+        }
+        const size_t lm = take((size_t)vl * H * esz), fnorm = take(H * esz), emb = take((size_t)c.vocab * H * esz);
+        wbytes = off;
+        LLMI_HIP(hipMalloc(&wblob, wbytes));
+        layers.resize(c.layers);
+        for (int l = 0; l < c.layers; ++l) {
+            Layer& L = layers[l];
+            L.qkv = wblob + lo[l].qkv;
+            L.o = wblob + lo[l].o;
+            L.gu = wblob + lo[l].gu;
+            L.down = wblob + lo[l].down;
+            if (wdt == LLMI_I8) {
+                L.qkv_s = (__half*)(wblob + lo[l].qs);
+                L.o_s = (__half*)(wblob + lo[l].os);
+                L.gu_s = (__half*)(wblob + lo[l].gs);
+                L.down_s = (__half*)(wblob + lo[l].ds);
+            }
+            L.attn_norm = wblob + lo[l].an;
+            L.ffn_norm = wblob + lo[l].fn;
+        }
+        lm_head = wblob + lm;
+        final_norm = wblob + fnorm;
+        embed = wblob + emb;
+        // bytes streamed per forward: every linear weight (+scales), norms, lm_head, one embedding row
+        uint64_t per_layer = (qkv_rows * H + H * ql + 2 * il * H + H * il) * wsz + 2 * H * esz;
+        if (wdt == LLMI_I8) per_layer += (qkv_rows + H + 2 * il + H) * 2;
+        stream_bytes = per_layer * c.layers + (uint64_t)vl * H * esz + H * esz + H * esz;
+        return LLMI_OK;
+    }
+
+    int alloc_state() {
+        const size_t H = c.hidden;
+        kv_layer_elems = (size_t)kvl * c.max_seq * c.head_dim;
+        const size_t kvb = (size_t)c.layers * kv_layer_elems * dtype_size(c.kv_dtype);
+        LLMI_HIP(hipMalloc(&kcache, kvb));
+        LLMI_HIP(hipMalloc(&vcache, kvb));
+        LLMI_HIP(hipMemsetAsync(kcache, 0, kvb, stream));
+        LLMI_HIP(hipMemsetAsync(vcache, 0, kvb, stream));
+
+        GemvArgs lmargs = lm_args();
+        lm_grid = gemv_grid(lmargs);
+        const size_t A = 256;
+        size_t off = 0;
+        auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, A); return o; };
+        const size_t o_ws = take(attn_workspace_bytes(hl, c.head_dim, c.max_seq));  // counters first
+        const size_t o_st = take(sizeof(DecodeState));
+        const size_t o_x = take(H * 4), o_qkv = take((ql + 2 * kvrows) * 4), o_att = take(ql * 4);
+        const size_t o_act = take((size_t)il * 4), o_log = take((size_t)vl * 4);
+        const size_t o_par = take((size_t)lm_grid * 8);
+        const size_t o_pr = take((size_t)c.max_seq * 4), o_tok = take((size_t)(c.max_seq + 1) * 4);
+        LLMI_HIP(hipMalloc(&scratch, off));
+        LLMI_HIP(hipMemsetAsync(scratch, 0, off, stream));
+        attn_ws = scratch + o_ws;
+        st = (DecodeState*)(scratch + o_st);
+        x = (float*)(scratch + o_x);
+        qkv_buf = (float*)(scratch + o_qkv);
+        attn_out = (float*)(scratch + o_att);
+        act = (float*)(scratch + o_act);
+        logits = (float*)(scratch + o_log);
+        partials = (unsigned long long*)(scratch + o_par);
+        prompt = (int32_t*)(scratch + o_pr);
+        tokens = (int32_t*)(scratch + o_tok);
+        LLMI_HIP(hipStreamSynchronize(stream));
+        return LLMI_OK;
+    }
+
+    // ----------------------------------------------------------- weights
+    int load_synthetic(uint64_t sd) {
+        seed = sd;
+        const int H = c.hidden, r = c.tp_rank;
+        const int lin = (wdt == LLMI_I8) ? LLMI_SYN_INT8 : LLMI_SYN_LINEAR;
+        auto fill = [&](void* dst, size_t row_off, int kind, int dt, uint32_t tid, int rows, int cols, int row0,
+                        int col0, int ld) -> int {
+            char* p = (char*)dst + row_off * (size_t)cols * dtype_size(dt);
+            return synth_fill_launch(p, dt, kind, seed, tid, rows, cols, row0, col0, ld, stream);
+        };
+        for (int l = 0; l < c.layers; ++l) {
+            Layer& L = layers[l];
+            auto t = [&](uint32_t k) { return prng::layer_tid(l, k); };
+            // fused [q; k; v] rows of this rank's heads (layer_weights.cc:25 order)
+            LLMI_TRY(fill(L.qkv, 0, lin, wdt, t(prng::Q), ql, H, r * ql, 0, H));
+            LLMI_TRY(fill(L.qkv, ql, lin, wdt, t(prng::K), kvrows, H, r * kvrows, 0, H));
+            LLMI_TRY(fill(L.qkv, ql + kvrows, lin, wdt, t(prng::V), kvrows, H, r * kvrows, 0, H));
+            LLMI_TRY(fill(L.o, 0, lin, wdt, t(prng::O), H, ql, 0, r * ql, c.heads * c.head_dim));
+            // fused [gate; up] rows (layer_weights.cc:40 order)
+            LLMI_TRY(fill(L.gu, 0, lin, wdt, t(prng::GATE), il, H, r * il, 0, H));
+            LLMI_TRY(fill(L.gu, il, lin, wdt, t(prng::UP), il, H, r * il, 0, H));
+            LLMI_TRY(fill(L.down, 0, lin, wdt, t(prng::DOWN), H, il, 0, r * il, c.inter));
+            if (wdt == LLMI_I8) {
+                const int S = LLMI_SYN_INT8_SCALE;
+                LLMI_TRY(fill(L.qkv_s, 0, S, LLMI_F16, t(prng::Q), ql, 1, r * ql, 0, 1));
+                LLMI_TRY(fill(L.qkv_s, ql, S, LLMI_F16, t(prng::K), kvrows, 1, r * kvrows, 0, 1));
+                LLMI_TRY(fill(L.qkv_s, ql + kvrows, S, LLMI_F16, t(prng::V), kvrows, 1, r * kvrows, 0, 1));
+                LLMI_TRY(fill(L.o_s, 0, S, LLMI_F16, t(prng::O), H, 1, 0, 0, 1));
+                LLMI_TRY(fill(L.gu_s, 0, S, LLMI_F16, t(prng::GATE), il, 1, r * il, 0, 1));
+                LLMI_TRY(fill(L.gu_s, il, S, LLMI_F16, t(prng::UP), il, 1, r * il, 0, 1));
+                LLMI_TRY(fill(L.down_s, 0, S, LLMI_F16, t(prng::DOWN), H, 1, 0, 0, 1));
+            }
+            LLMI_TRY(fill(L.attn_norm, 0, LLMI_SYN_GAMMA, edt, t(prng::ATTN_NORM), 1, H, 0, 0, H));
+            LLMI_TRY(fill(L.ffn_norm, 0, LLMI_SYN_GAMMA, edt, t(prng::FFN_NORM), 1, H, 0, 0, H));
+        }
+        LLMI_TRY(fill(lm_head, 0, LLMI_SYN_LINEAR, edt, prng::LM_HEAD, vl, H, r * vl, 0, H));
+        LLMI_TRY(fill(final_norm, 0, LLMI_SYN_GAMMA, edt, prng::FINAL_NORM, 1, H, 0, 0, H));
+        LLMI_TRY(fill(embed, 0, LLMI_SYN_EMBED, edt, prng::EMBED, c.vocab, H, 0, 0, H));
+        LLMI_HIP(hipStreamSynchronize(stream));
+        return LLMI_OK;
+    }
+
+    // ---------------------------------------------------------- one token
+    GemvArgs lm_args() const {
+        GemvArgs a;
+        a.w = lm_head;
+        a.w_dtype = edt;
+        a.n_rows = vl;
+        a.k = c.hidden;
+        a.x = x;
+        a.gamma = final_norm;
+        a.g_dtype = edt;
+        a.eps = c.rms_eps;
+        a.epi = EPI_ARGMAX;
+        a.y = logits;
+        a.partials = partials;
+        a.idx_base = (uint32_t)(c.tp_rank * vl);
+        return a;
+    }
+
+    GemvArgs qkv_args(int l) const {
+        const Layer& L = layers[l];
+        GemvArgs a;
+        a.w = L.qkv; a.scales = L.qkv_s; a.w_dtype = wdt;
+        a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
+        a.x = x; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
+        a.epi = EPI_STORE; a.y = qkv_buf;
+        return a;
+    }
+    AttnArgs attn_args(int l) const {
+        AttnArgs a;
+        const size_t eb = dtype_size(c.kv_dtype);
+        a.qkv = qkv_buf;
+        a.k_cache = (char*)kcache + (size_t)l * kv_layer_elems * eb;
+        a.v_cache = (char*)vcache + (size_t)l * kv_layer_elems * eb;
+        a.cache_dtype = c.kv_dtype;
+        a.max_seq = c.max_seq;
+        a.pos_dev = &st->cur_pos;
+        a.heads = hl; a.kv_heads = kvl; a.head_dim = c.head_dim;
+        a.rope = 1; a.rope_base = c.rope_base;
+        a.out = attn_out; a.workspace = attn_ws;
+        return a;
+    }
+    GemvArgs o_args(int l) const {
+        const Layer& L = layers[l];
+        GemvArgs a;
+        a.w = L.o; a.scales = L.o_s; a.w_dtype = wdt;
+        a.n_rows = c.hidden; a.k = ql; a.x = attn_out;
+        a.epi = (c.tp_rank == 0) ? EPI_ADD : EPI_STORE;  // rank 0 carries the residual into the all-reduce
+        a.y = x; a.resid = x;
+        return a;
+    }
+    GemvArgs gu_args(int l) const {
+        const Layer& L = layers[l];
+        GemvArgs a;
+        a.w = L.gu; a.scales = L.gu_s; a.w_dtype = wdt;
+        a.n_rows = 2 * il; a.k = c.hidden;
+        a.x = x; a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
+        a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
+        return a;
+    }
+    GemvArgs down_args(int l) const {
+        const Layer& L = layers[l];
+        GemvArgs a;
+        a.w = L.down; a.scales = L.down_s; a.w_dtype = wdt;
+        a.n_rows = c.hidden; a.k = il; a.x = act;
+        a.epi = (c.tp_rank == 0) ? EPI_ADD : EPI_STORE;
+        a.y = x; a.resid = x;
+        return a;
+    }
+
+    int allreduce_sum(float* buf, size_t n) {
+        if (!comm) return LLMI_OK;
+        ncclResult_t r = ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, stream);
+        LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        return LLMI_OK;
+    }
+
+    int record_step() {
+        LLMI_TRY(step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, c.max_seq,
+                                   stream));
+        for (int l = 0; l < c.layers; ++l) {
+            LLMI_TRY(gemv_launch(qkv_args(l), stream));
+            LLMI_TRY(attn_decode_launch(attn_args(l), stream));
+            LLMI_TRY(gemv_launch(o_args(l), stream));
+            LLMI_TRY(allreduce_sum(x, c.hidden));
+            LLMI_TRY(gemv_launch(gu_args(l), stream));
+            LLMI_TRY(gemv_launch(down_args(l), stream));
+            LLMI_TRY(allreduce_sum(x, c.hidden));
+        }
+        LLMI_TRY(gemv_launch(lm_args(), stream));
+        if (comm) {
+            ncclResult_t r = ncclAllReduce(partials, partials, lm_grid, ncclUint64, ncclMax, comm, stream);
+            LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(max): ") + ncclGetErrorString(r));
+        }
+        return LLMI_OK;
+    }
+
+    int build_graph() {
+        if (exec) return LLMI_OK;
+        LLMI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        int rc = record_step();
+        hipGraph_t g = nullptr;
+        hipError_t e = hipStreamEndCapture(stream, &g);
+        if (rc != LLMI_OK) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        LLMI_HIP(e);
+        graph = g;
+        LLMI_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        return LLMI_OK;
+    }
+
+    // ------------------------------------------------------------- driving
+    int set_prompt(const int32_t* ids, int n) {
+        LLMI_REQUIRE(ids && n >= 1 && n <= c.max_seq, "set_prompt: need 1 <= n <= max_seq ids");
+        for (int i = 0; i < n; ++i)
+            LLMI_REQUIRE(ids[i] >= 0 && ids[i] < c.vocab, "set_prompt: token id out of range");
+        DecodeState h{};
+        h.next_pos = 0;
+        h.cur_pos = 0;
+        h.prompt_len = n;
+        h.vocab = c.vocab;
+        h.error = 0;
+        LLMI_HIP(hipMemcpyAsync(prompt, ids, (size_t)n * 4, hipMemcpyHostToDevice, stream));
+        LLMI_HIP(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, stream));
+        LLMI_HIP(hipStreamSynchronize(stream));
+        host_next_pos = 0;
+        prompt_len = n;
+        return LLMI_OK;
+    }
+
+    int decode(int n, int use_graph) {
+        LLMI_REQUIRE(prompt_len > 0, "decode: set_prompt first");
+        LLMI_REQUIRE(n >= 0 && host_next_pos + n <= c.max_seq, "decode: would run past max_seq");
+        if (use_graph) LLMI_TRY(build_graph());
+        for (int i = 0; i < n; ++i) {
+            if (use_graph)
+                LLMI_HIP(hipGraphLaunch(exec, stream));
+            else
+                LLMI_TRY(record_step());
+        }
+        host_next_pos += n;
+        return LLMI_OK;
+    }
+
+    int tokens_out(int32_t* out, int n, int* n_valid) {
+        int valid = host_next_pos;
+        if (host_next_pos >= prompt_len && host_next_pos < c.max_seq) {
+            LLMI_TRY(finalize_launch(st, partials, lm_grid, tokens, c.max_seq, stream));
+            valid = host_next_pos + 1;
+        }
+        LLMI_HIP(hipStreamSynchronize(stream));
+        DecodeState h;
+        LLMI_HIP(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
+        LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error));
+        const int m = n < valid ? n : valid;
+        if (m > 0) LLMI_HIP(hipMemcpy(out, tokens, (size_t)m * 4, hipMemcpyDeviceToHost));
+        if (n_valid) *n_valid = valid;
+        return LLMI_OK;
+    }
+};
+
+}  // namespace llmi
+
+// ============================================================== C ABI (engine)
+using llmi::Engine;
+struct llmi_engine {
+    Engine e;
+};
+
+namespace {
+float h2f(uint16_t h) {
+    __half v;
+    std::memcpy(&v, &h, 2);
+    return __half2float(v);
+}
+}  // namespace
+
+extern "C" {
+
+int llmi_config_preset(const char* name, llmi_config* cfg) {
+    LLMI_REQUIRE(name && cfg, "preset: null argument");
+    llmi_config c{};
+    c.hidden = 4096; c.heads = 32; c.kv_heads = 32; c.head_dim = 128; c.inter = 11008;
+    c.layers = 32; c.vocab = 32000; c.max_seq = 2048; c.rms_eps = 1e-5f; c.rope_base = 10000.f;
+    c.weight_dtype = LLMI_F16; c.kv_dtype = LLMI_F16; c.tp_rank = 0; c.tp_world = 1;
+    const std::string n(name);
+    if (n == "llama2-7b") {
+    } else if (n == "llama2-13b") {
+        c.hidden = 5120; c.heads = 40; c.kv_heads = 40; c.inter = 13824; c.layers = 40;
+    } else if (n == "tiny") {
+        c.hidden = 512; c.heads = 4; c.kv_heads = 4; c.inter = 1024; c.layers = 2; c.max_seq = 64;
+    } else {
+        LLMI_REQUIRE(false, "preset: unknown name " + n);
+    }
+    *cfg = c;
+    return LLMI_OK;
+}
+
+int llmi_tp_unique_id(void* out128) {
+    LLMI_REQUIRE(out128, "tp_unique_id: null");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    LLMI_REQUIRE(r == ncclSuccess, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    static_assert(sizeof(id) == 128, "ncclUniqueId must be 128 bytes");
+    std::memcpy(out128, &id, sizeof(id));
+    return LLMI_OK;
+}
+
+int llmi_engine_create(const llmi_config* cfg, int device, const void* tp_id, llmi_engine** out) {
+    LLMI_REQUIRE(cfg && out, "engine_create: null argument");
+    *out = nullptr;
+    auto h = std::make_unique<llmi_engine>();
+    int rc = h->e.init(*cfg, device, tp_id);
+    if (rc != LLMI_OK) return rc;
+    *out = h.release();
+    return LLMI_OK;
+}
+
+int llmi_engine_destroy(llmi_engine* e) {
+    if (e) {
+        (void)hipSetDevice(e->e.device);
+        (void)hipStreamSynchronize(e->e.stream);
+        delete e;
+    }
+    return LLMI_OK;
+}
+
+int llmi_engine_load_synthetic(llmi_engine* e, uint64_t seed) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.load_synthetic(seed);
+}
+
+int llmi_engine_set_prompt(llmi_engine* e, const int32_t* ids, int n) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.set_prompt(ids, n);
+}
+
+int llmi_engine_decode(llmi_engine* e, int n_steps, int use_graph) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.decode(n_steps, use_graph);
+}
+
+int llmi_engine_sync(llmi_engine* e) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipStreamSynchronize(e->e.stream));
+    return LLMI_OK;
+}
+
+int llmi_engine_tokens(llmi_engine* e, int32_t* out, int n, int* n_valid) {
+    LLMI_REQUIRE(e && (out || n == 0), "null argument");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.tokens_out(out, n, n_valid);
+}
+
+int llmi_engine_logits(llmi_engine* e, float* out, int n) {
+    LLMI_REQUIRE(e && out && n <= e->e.vl, "engine_logits: bad arguments");
+    LLMI_HIP(hipStreamSynchronize(e->e.stream));
+    LLMI_HIP(hipMemcpy(out, e->e.logits, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return LLMI_OK;
+}
+
+int llmi_engine_hidden(llmi_engine* e, float* out, int n) {
+    LLMI_REQUIRE(e && out && n <= e->e.c.hidden, "engine_hidden: bad arguments");
+    LLMI_HIP(hipStreamSynchronize(e->e.stream));
+    LLMI_HIP(hipMemcpy(out, e->e.x, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return LLMI_OK;
+}
+
+int llmi_engine_kv_slot(llmi_engine* e, int layer, int pos, int which_v, float* out) {
+    LLMI_REQUIRE(e && out, "kv_slot: null argument");
+    Engine& g = e->e;
+    LLMI_REQUIRE(layer >= 0 && layer < g.c.layers && pos >= 0 && pos < g.c.max_seq, "kv_slot: out of range");
+    LLMI_HIP(hipStreamSynchronize(g.stream));
+    const size_t eb = llmi::dtype_size(g.c.kv_dtype), D = g.c.head_dim;
+    const char* base = (const char*)(which_v ? g.vcache : g.kcache) + (size_t)layer * g.kv_layer_elems * eb;
+    std::vector<char> tmp(D * eb);
+    for (int h = 0; h < g.kvl; ++h) {
+        LLMI_HIP(hipMemcpy(tmp.data(), base + ((size_t)h * g.c.max_seq + pos) * D * eb, D * eb,
+                           hipMemcpyDeviceToHost));
+        for (size_t d = 0; d < D; ++d) {
+            if (g.c.kv_dtype == LLMI_F32)
+                std::memcpy(out + h * D + d, tmp.data() + d * 4, 4);
+            else
+                out[h * D + d] = h2f(*reinterpret_cast<uint16_t*>(tmp.data() + d * 2));
+        }
+    }
+    return LLMI_OK;
+}
+
+int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes_per_pos) {
+    LLMI_REQUIRE(e, "null engine");
+    const Engine& g = e->e;
+    if (weight_bytes) *weight_bytes = g.stream_bytes;
+    if (kv_bytes_per_pos)
+        *kv_bytes_per_pos = (uint64_t)g.c.layers * g.kvl * g.c.head_dim * 2 * llmi::dtype_size(g.c.kv_dtype);
+    return LLMI_OK;
+}
+
+llmi_stream_t llmi_engine_stream(llmi_engine* e) { return e ? (llmi_stream_t)e->e.stream : nullptr; }
+
+int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes) {
+    LLMI_REQUIRE(e && avg_us && iters > 0, "time_kernel: bad arguments");
+    Engine& g = e->e;
+    LLMI_HIP(hipSetDevice(g.device));
+    LLMI_REQUIRE(g.prompt_len > 0 && g.host_next_pos > 0, "time_kernel: decode at least one step first");
+    const size_t H = g.c.hidden;
+    uint64_t b = 0;
+    auto launch = [&]() -> int {
+        switch (which) {
+            case 0: return llmi::gemv_launch(g.qkv_args(0), g.stream);
+            case 1: return llmi::attn_decode_launch(g.attn_args(0), g.stream);
+            case 2: return llmi::gemv_launch(g.o_args(0), g.stream);
+            case 3: return llmi::gemv_launch(g.gu_args(0), g.stream);
+            case 4: return llmi::gemv_launch(g.down_args(0), g.stream);
+            case 5: return llmi::gemv_launch(g.lm_args(), g.stream);
+        }
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..5");
+    };
+    const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
+    switch (which) {
+        case 0: b = (uint64_t)(g.ql + 2 * g.kvrows) * H * ws + (g.ql + 2 * g.kvrows) * sc; break;
+        case 1: {
+            llmi::DecodeState hs;
+            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
+            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
+            b = (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb;
+            break;
+        }
+        case 2: b = (uint64_t)H * g.ql * ws + H * sc; break;
+        case 3: b = (uint64_t)2 * g.il * H * ws + 2 * g.il * sc; break;
+        case 4: b = (uint64_t)H * g.il * ws + H * sc; break;
+        case 5: b = (uint64_t)g.vl * H * g.esz; break;
+    }
+    // timing launches modify the residual stream (o/down epilogues add into x),
+    // so save and restore the small activation state around them
+    std::vector<char> save(H * 4);
+    LLMI_HIP(hipMemcpyAsync(save.data(), g.x, H * 4, hipMemcpyDeviceToHost, g.stream));
+    LLMI_TRY(launch());  // warm
+    hipEvent_t t0, t1;
+    LLMI_HIP(hipEventCreate(&t0));
+    LLMI_HIP(hipEventCreate(&t1));
+    LLMI_HIP(hipEventRecord(t0, g.stream));
+    for (int i = 0; i < iters; ++i) LLMI_TRY(launch());
+    LLMI_HIP(hipEventRecord(t1, g.stream));
+    LLMI_HIP(hipEventSynchronize(t1));
+    float ms = 0.f;
+    LLMI_HIP(hipEventElapsedTime(&ms, t0, t1));
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    LLMI_HIP(hipMemcpy(g.x, save.data(), H * 4, hipMemcpyHostToDevice));
+    *avg_us = ms * 1000.f / iters;
+    if (bytes) *bytes = b;
+    return LLMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,100 @@
+// Internal kernel launch interface (C++). The public C ABI (include/llmi.h)
+// and the decode engine (engine.hip) are both built on these.
+#pragma once
+#include "common.h"
+
+namespace llmi {
+
+// ------------------------------------------------------------------ GEMV
+enum GemvEpi : int {
+    EPI_STORE = 0,     // y[r] = acc
+    EPI_ADD = 1,       // y[r] = acc + resid_scale * resid[r]   (resid may alias y)
+    EPI_SILU_MUL = 2,  // rows (g, g + pair_off): y[g] = silu(acc0) * acc1
+    EPI_ARGMAX = 3,    // y[r] = acc; per-block argmax key -> partials[blockIdx]
+};
+
+struct GemvArgs {
+    const void* w = nullptr;       // [n_rows, k] row-major, dtype w_dtype
+    const __half* scales = nullptr;  // int8: per-row fp16 scale
+    int w_dtype = LLMI_F16;
+    int n_rows = 0;                // rows of W
+    int k = 0;
+    const float* x = nullptr;      // [k]
+    // prologue: optional RMSNorm of x (gamma dtype g_dtype), x_add: x += x_add first
+    const void* gamma = nullptr;
+    int g_dtype = LLMI_F16;
+    float eps = 1e-5f;
+    // epilogue
+    int epi = EPI_STORE;
+    float* y = nullptr;
+    const float* resid = nullptr;
+    float resid_scale = 1.f;
+    int pair_off = 0;              // EPI_SILU_MUL: row offset of the `up` row
+    unsigned long long* partials = nullptr;  // EPI_ARGMAX: [grid]
+    uint32_t idx_base = 0;         // EPI_ARGMAX: global index of row 0 (vocab shard)
+    int grid = 0;                  // 0 = auto
+};
+
+int gemv_launch(const GemvArgs& a, hipStream_t s);
+int gemv_grid(const GemvArgs& a);  // blocks gemv_launch will use
+
+// ------------------------------------------------------------- attention
+struct AttnArgs {
+    const float* qkv = nullptr;    // [(heads + 2 kv_heads) * D]
+    void* k_cache = nullptr;       // layer base: [kv_heads, max_seq, D]
+    void* v_cache = nullptr;
+    int cache_dtype = LLMI_F16;
+    int max_seq = 0;
+    const int* pos_dev = nullptr;  // device position (engine); else pos_host
+    int pos_host = 0;
+    int heads = 0, kv_heads = 0, head_dim = 128;
+    int rope = 1;
+    float rope_base = 10000.f;
+    float* out = nullptr;          // [heads * D]
+    void* workspace = nullptr;
+};
+constexpr int kAttnChunk = 64;     // cached positions per workgroup (split-KV)
+size_t attn_workspace_bytes(int heads, int head_dim, int max_seq);
+int attn_decode_launch(const AttnArgs& a, hipStream_t s);
+
+// ------------------------------------------------------ decode-loop state
+struct DecodeState {
+    int next_pos;     // position the next forward will process
+    int cur_pos;      // position of the forward in flight
+    int prompt_len;
+    int vocab;
+    int error;        // sticky error flags (1: token id out of range, 2: position overflow)
+    int pad[3];
+};
+
+// step start: pick the token for position next_pos (prompt id or argmax of
+// the previous forward's partials), record it, gather its embedding row.
+int step_start_launch(DecodeState* st, const int32_t* prompt, const unsigned long long* partials,
+                      int n_partials, int32_t* tokens, const void* table, int table_dtype, int hidden,
+                      float* x, int max_seq, hipStream_t s);
+// after the last forward: tokens[next_pos] = argmax(partials) (no state change)
+int finalize_launch(DecodeState* st, const unsigned long long* partials, int n_partials,
+                    int32_t* tokens, int max_seq, hipStream_t s);
+
+// ------------------------------------------------------- elementwise ops
+int embedding_launch(const int32_t* ids, int n, const void* table, int t_dtype, int vocab, int hidden,
+                     float* out, hipStream_t s);
+int rmsnorm_launch(const float* x, float* out, float* resid_out, const void* gamma, int g_dtype,
+                   int n, int hidden, float eps, hipStream_t s);
+int add_resid_rmsnorm_launch(float* resid, float* out, const void* bias, int b_dtype,
+                             const void* gamma, int g_dtype, int n, int hidden, float eps,
+                             hipStream_t s);
+int add_resid_launch(const float* resid, float* out, int n, int hidden, hipStream_t s);
+int silu_mul_launch(const float* gu, float* out, int n, int inter, hipStream_t s);
+int rope_decode_launch(float* qkv, int pos, int heads, int kv_heads, int head_dim, float base,
+                       hipStream_t s);
+int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long long* scratch,
+                  hipStream_t s);
+
+// ---------------------------------------------------------- synthetic
+int synth_fill_launch(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
+                      int cols, int row0, int col0, int ld, hipStream_t s);
+int synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
+                    int cols, int row0, int col0, int ld);
+
+}  // namespace llmi

@@ -1,0 +1,362 @@
+// Small memory-bound ops of the decode path (one launch each in the operator
+// API; fused into the GEMV/attention kernels inside the engine) plus the
+// device-side token loop (step start / greedy argmax) and the synthetic-weight
+// generator.
+#include <cmath>
+#include <cstring>
+
+#include "kernels.h"
+#include "prng.h"
+
+namespace llmi {
+namespace {
+
+constexpr int kT = 256;
+
+template <typename T>
+__device__ __forceinline__ float ld(const void* p, size_t i) {
+    return to_f32(reinterpret_cast<const T*>(p)[i]);
+}
+__device__ __forceinline__ float ldg(const void* p, int dt, size_t i) {
+    return dt == LLMI_F16 ? ld<__half>(p, i) : ld<float>(p, i);
+}
+
+// launchInputEmbedding (input_embedding.cu:4-50): row gather, fp32 out.
+template <typename TT>
+__global__ void embedding_kernel(const int32_t* ids, const TT* table, int vocab, int hidden, float* out,
+                                 int* err) {
+    const int t = blockIdx.y;
+    int id = ids[t];
+    if (id < 0 || id >= vocab) {
+        if (threadIdx.x == 0 && blockIdx.x == 0 && err) atomicOr(err, 1);
+        id = 0;
+    }
+    const TT* row = table + (size_t)id * hidden;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < hidden; i += gridDim.x * blockDim.x)
+        out[(size_t)t * hidden + i] = to_f32(row[i]);
+}
+
+// launchRMSNorm (rmsnorm_kernel.cu:62-204) semantics of modeling_llama.py:112-117.
+__global__ void rmsnorm_kernel(const float* x, float* out, float* resid_out, const void* gamma, int g_dt,
+                               int hidden, float eps) {
+    __shared__ float red[16];
+    const float* xr = x + (size_t)blockIdx.x * hidden;
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < hidden; i += blockDim.x) ss += xr[i] * xr[i];
+    ss = block_sum(ss, red);
+    const float rstd = 1.0f / sqrtf(ss / (float)hidden + eps);
+    for (int i = threadIdx.x; i < hidden; i += blockDim.x) {
+        const float v = xr[i];
+        if (resid_out) resid_out[(size_t)blockIdx.x * hidden + i] = v;
+        out[(size_t)blockIdx.x * hidden + i] = ldg(gamma, g_dt, i) * (v * rstd);
+    }
+}
+
+// launchFusedAddBiasResidualRMSNorm (fused_addresidual_norm.cu:61-221).
+__global__ void add_resid_rmsnorm_kernel(float* resid, float* out, const void* bias, int b_dt,
+                                         const void* gamma, int g_dt, int hidden, float eps) {
+    __shared__ float red[16];
+    float* r = resid + (size_t)blockIdx.x * hidden;
+    float* o = out + (size_t)blockIdx.x * hidden;
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < hidden; i += blockDim.x) {
+        float v = r[i] + o[i] + (bias ? ldg(bias, b_dt, i) : 0.f);
+        r[i] = v;
+        ss += v * v;
+    }
+    ss = block_sum(ss, red);
+    const float rstd = 1.0f / sqrtf(ss / (float)hidden + eps);
+    for (int i = threadIdx.x; i < hidden; i += blockDim.x) o[i] = ldg(gamma, g_dt, i) * (r[i] * rstd);
+}
+
+__global__ void add_resid_kernel(const float* resid, float* out, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] += resid[i];
+}
+
+// launchAct (act_kernel.cu:17-74): in [n, 2, inter] gate first, up second.
+__global__ void silu_mul_kernel(const float* gu, float* out, int inter) {
+    const float* g = gu + (size_t)blockIdx.y * 2 * inter;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < inter; i += gridDim.x * blockDim.x) {
+        const float v = g[i];
+        out[(size_t)blockIdx.y * inter + i] = v / (1.0f + expf(-v)) * g[inter + i];
+    }
+}
+
+// launchRoPE (qkv_bias_and_RoPE.cu:322-451) with HF angle arithmetic
+// (modeling_llama.py:123-146, 204-235): one block per q/k head.
+__global__ void rope_decode_kernel(float* qkv, int pos, int heads, int kv_heads, int d, float base) {
+    const int h = blockIdx.x;  // 0 .. heads + kv_heads - 1 (q heads then k heads)
+    float* x = qkv + (size_t)h * d;
+    for (int i = threadIdx.x; i < d / 2; i += blockDim.x) {
+        const float p = (float)pow((double)base, (double)(2 * i) / (double)d);
+        const float ang = __fmul_rn((float)pos, __fdiv_rn(1.0f, p));
+        double sd, cd;
+        sincos((double)ang, &sd, &cd);
+        const float c = (float)cd, s = (float)sd;
+        const float x0 = x[i], x1 = x[i + d / 2];
+        x[i] = x0 * c - x1 * s;
+        x[i + d / 2] = x1 * c + x0 * s;
+    }
+}
+
+// ------------------------------------------------- greedy argmax (two phase)
+__device__ unsigned long long block_max_key(unsigned long long k, unsigned long long* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_xor(k, off, kWave);
+        k = o > k ? o : k;
+    }
+    __syncthreads();
+    if (lane == 0) sh[w] = k;
+    __syncthreads();
+    unsigned long long b = sh[0];
+    for (int i = 1; i < nw; ++i) b = sh[i] > b ? sh[i] : b;
+    return b;
+}
+
+__global__ void argmax_partial_kernel(const float* logits, int n, unsigned long long* partials) {
+    __shared__ unsigned long long sh[16];
+    unsigned long long best = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        unsigned long long k = argmax_key(logits[i], (uint32_t)i);
+        best = k > best ? k : best;
+    }
+    best = block_max_key(best, sh);
+    if (threadIdx.x == 0) partials[blockIdx.x] = best;
+}
+
+__global__ void argmax_final_kernel(const unsigned long long* partials, int np, int32_t* out) {
+    __shared__ unsigned long long sh[16];
+    unsigned long long best = 0;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) best = partials[i] > best ? partials[i] : best;
+    best = block_max_key(best, sh);
+    if (threadIdx.x == 0) *out = (int32_t)argmax_key_index(best);
+}
+
+// ---------------------------------------------------- device token loop
+// One forward's first kernel (Llama<T>::continueTokenGen, llama.cpp:318-349 +
+// the Response loop's token hand-off, llama.cpp:411-446, with no host round trip):
+// choose the token of position next_pos, record it, gather its embedding.
+template <typename TT>
+__global__ void step_start_kernel(DecodeState* st, const int32_t* prompt, const unsigned long long* partials,
+                                  int np, int32_t* tokens, const TT* table, int hidden, float* x, int max_seq) {
+    __shared__ unsigned long long sh[16];
+    __shared__ int tok_s;
+    const int p = st->next_pos;
+    if (p >= max_seq) {  // host guards this; keep the state consistent if it does not
+        if (threadIdx.x == 0) atomicOr(&st->error, 2);
+        return;
+    }
+    int tok;
+    if (p < st->prompt_len) {
+        tok = prompt[p];
+    } else {
+        unsigned long long best = 0;
+        for (int i = threadIdx.x; i < np; i += blockDim.x) best = partials[i] > best ? partials[i] : best;
+        best = block_max_key(best, sh);
+        tok = (int)argmax_key_index(best);
+    }
+    if (threadIdx.x == 0) {
+        if (tok < 0 || tok >= st->vocab) {
+            atomicOr(&st->error, 1);
+            tok = 0;
+        }
+        tok_s = tok;
+    }
+    __syncthreads();
+    tok = tok_s;
+    if (threadIdx.x == 0) {
+        tokens[p] = tok;
+        st->cur_pos = p;
+        st->next_pos = p + 1;
+    }
+    const TT* row = table + (size_t)tok * hidden;
+    for (int i = threadIdx.x; i < hidden; i += blockDim.x) x[i] = to_f32(row[i]);
+}
+
+__global__ void finalize_kernel(DecodeState* st, const unsigned long long* partials, int np, int32_t* tokens,
+                                int max_seq) {
+    __shared__ unsigned long long sh[16];
+    const int p = st->next_pos;
+    unsigned long long best = 0;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) best = partials[i] > best ? partials[i] : best;
+    best = block_max_key(best, sh);
+    if (threadIdx.x == 0 && p < max_seq && p >= st->prompt_len) tokens[p] = (int)argmax_key_index(best);
+}
+
+// ------------------------------------------------------ synthetic weights
+struct SynthDesc {
+    int kind, out_dtype, rows, cols, row0, col0, ld;
+    uint64_t key;
+};
+
+__host__ __device__ inline void synth_one(const SynthDesc& d, void* out, size_t li, int r, int c) {
+    const uint64_t gi = (uint64_t)(d.row0 + r) * (uint64_t)d.ld + (uint64_t)(d.col0 + c);
+    switch (d.kind) {
+        case LLMI_SYN_LINEAR:
+        case LLMI_SYN_EMBED:
+        case LLMI_SYN_GAMMA: {
+            const float f = d.kind == LLMI_SYN_LINEAR ? prng::linear_f32(d.key, gi)
+                            : d.kind == LLMI_SYN_EMBED ? prng::embed_f32(d.key, gi)
+                                                       : prng::gamma_f32(d.key, gi);
+            const __half h = __float2half(f);  // RNE; the fp32 output keeps the fp16 value
+            if (d.out_dtype == LLMI_F16)
+                reinterpret_cast<__half*>(out)[li] = h;
+            else
+                reinterpret_cast<float*>(out)[li] = __half2float(h);
+            break;
+        }
+        case LLMI_SYN_INT8:
+            reinterpret_cast<int8_t*>(out)[li] = prng::int8_w(d.key, gi);
+            break;
+        case LLMI_SYN_INT8_SCALE:
+            reinterpret_cast<__half*>(out)[li] = __float2half(prng::int8_scale_f32(d.key, gi));
+            break;
+    }
+}
+
+__global__ void synth_kernel(SynthDesc d, void* out) {
+    const size_t n = (size_t)d.rows * d.cols;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(i / d.cols), c = (int)(i % d.cols);
+        synth_one(d, out, i, r, c);
+    }
+}
+
+int synth_desc(SynthDesc* d, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows, int cols,
+               int row0, int col0, int ld) {
+    LLMI_REQUIRE(rows >= 0 && cols >= 0 && row0 >= 0 && col0 >= 0, "synth: negative extent");
+    LLMI_REQUIRE(kind >= LLMI_SYN_LINEAR && kind <= LLMI_SYN_INT8_SCALE, "synth: bad kind");
+    if (kind == LLMI_SYN_INT8) LLMI_REQUIRE(out_dtype == LLMI_I8, "synth: int8 weights need I8 output");
+    else if (kind == LLMI_SYN_INT8_SCALE) LLMI_REQUIRE(out_dtype == LLMI_F16, "synth: scales are F16");
+    else LLMI_REQUIRE(out_dtype == LLMI_F16 || out_dtype == LLMI_F32, "synth: output must be F16 or F32");
+    d->kind = kind;
+    d->out_dtype = out_dtype;
+    d->rows = rows;
+    d->cols = cols;
+    d->row0 = row0;
+    d->col0 = col0;
+    d->ld = ld > 0 ? ld : cols;
+    // gamma uses the element index directly (ld = hidden, rows = 1); int8 scales
+    // index rows (cols = 1, ld = 1) and live under tensor id tid | Q_SCALE
+    const uint32_t t = kind == LLMI_SYN_INT8_SCALE ? (tid | prng::Q_SCALE) : tid;
+    d->key = prng::tensor_key(seed, t);
+    return LLMI_OK;
+}
+
+}  // namespace
+
+int embedding_launch(const int32_t* ids, int n, const void* table, int t_dtype, int vocab, int hidden,
+                     float* out, hipStream_t s) {
+    LLMI_REQUIRE(ids && table && out && n > 0 && hidden > 0 && vocab > 0, "embedding: bad arguments");
+    const dim3 grid((hidden + kT - 1) / kT, n);
+    if (t_dtype == LLMI_F16)
+        hipLaunchKernelGGL(embedding_kernel<__half>, grid, dim3(kT), 0, s, ids, (const __half*)table, vocab,
+                           hidden, out, nullptr);
+    else if (t_dtype == LLMI_F32)
+        hipLaunchKernelGGL(embedding_kernel<float>, grid, dim3(kT), 0, s, ids, (const float*)table, vocab,
+                           hidden, out, nullptr);
+    else
+        LLMI_REQUIRE(false, "embedding: table dtype must be f16 or f32");
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int rmsnorm_launch(const float* x, float* out, float* resid_out, const void* gamma, int g_dtype, int n,
+                   int hidden, float eps, hipStream_t s) {
+    LLMI_REQUIRE(x && out && gamma && n > 0 && hidden > 0, "rmsnorm: bad arguments");
+    LLMI_REQUIRE(g_dtype == LLMI_F16 || g_dtype == LLMI_F32, "rmsnorm: gamma must be f16/f32");
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3(n), dim3(kT), 0, s, x, out, resid_out, gamma, g_dtype, hidden, eps);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int add_resid_rmsnorm_launch(float* resid, float* out, const void* bias, int b_dtype, const void* gamma,
+                             int g_dtype, int n, int hidden, float eps, hipStream_t s) {
+    LLMI_REQUIRE(resid && out && gamma && n > 0 && hidden > 0, "add_residual_rmsnorm: bad arguments");
+    hipLaunchKernelGGL(add_resid_rmsnorm_kernel, dim3(n), dim3(kT), 0, s, resid, out, bias, b_dtype, gamma,
+                       g_dtype, hidden, eps);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int add_resid_launch(const float* resid, float* out, int n, int hidden, hipStream_t s) {
+    LLMI_REQUIRE(resid && out && n > 0 && hidden > 0, "add_residual: bad arguments");
+    const size_t total = (size_t)n * hidden;
+    const int grid = (int)std::min<size_t>((total + kT - 1) / kT, 4096);
+    hipLaunchKernelGGL(add_resid_kernel, dim3(grid), dim3(kT), 0, s, resid, out, total);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int silu_mul_launch(const float* gu, float* out, int n, int inter, hipStream_t s) {
+    LLMI_REQUIRE(gu && out && n > 0 && inter > 0, "silu_mul: bad arguments");
+    hipLaunchKernelGGL(silu_mul_kernel, dim3((inter + kT - 1) / kT, n), dim3(kT), 0, s, gu, out, inter);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int rope_decode_launch(float* qkv, int pos, int heads, int kv_heads, int head_dim, float base, hipStream_t s) {
+    LLMI_REQUIRE(qkv && heads > 0 && kv_heads > 0 && head_dim > 0 && head_dim % 2 == 0 && pos >= 0,
+                 "rope: bad arguments");
+    hipLaunchKernelGGL(rope_decode_kernel, dim3(heads + kv_heads), dim3(64), 0, s, qkv, pos, heads, kv_heads,
+                       head_dim, base);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long long* scratch, hipStream_t s) {
+    LLMI_REQUIRE(logits && out_id && scratch && n > 0, "argmax: bad arguments");
+    const int grid = std::min((n + kT - 1) / kT, 256);
+    hipLaunchKernelGGL(argmax_partial_kernel, dim3(grid), dim3(kT), 0, s, logits, n, scratch);
+    hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(kT), 0, s, scratch, grid, out_id);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int step_start_launch(DecodeState* st, const int32_t* prompt, const unsigned long long* partials, int np,
+                      int32_t* tokens, const void* table, int t_dtype, int hidden, float* x, int max_seq,
+                      hipStream_t s) {
+    if (t_dtype == LLMI_F16)
+        hipLaunchKernelGGL(step_start_kernel<__half>, dim3(1), dim3(1024), 0, s, st, prompt, partials, np, tokens,
+                           (const __half*)table, hidden, x, max_seq);
+    else
+        hipLaunchKernelGGL(step_start_kernel<float>, dim3(1), dim3(1024), 0, s, st, prompt, partials, np, tokens,
+                           (const float*)table, hidden, x, max_seq);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int finalize_launch(DecodeState* st, const unsigned long long* partials, int np, int32_t* tokens, int max_seq,
+                    hipStream_t s) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, st, partials, np, tokens, max_seq);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int synth_fill_launch(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows, int cols,
+                      int row0, int col0, int ld, hipStream_t s) {
+    SynthDesc d;
+    LLMI_TRY(synth_desc(&d, out_dtype, kind, seed, tid, rows, cols, row0, col0, ld));
+    LLMI_REQUIRE(out != nullptr, "synth: null output");
+    const size_t n = (size_t)rows * cols;
+    if (n == 0) return LLMI_OK;
+    const int grid = (int)std::min<size_t>((n + kT - 1) / kT, 8192);
+    hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(kT), 0, s, d, out);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows, int cols,
+                    int row0, int col0, int ld) {
+    SynthDesc d;
+    LLMI_TRY(synth_desc(&d, out_dtype, kind, seed, tid, rows, cols, row0, col0, ld));
+    LLMI_REQUIRE(out != nullptr, "synth: null output");
+    for (int r = 0; r < rows; ++r)
+        for (int c = 0; c < cols; ++c) synth_one(d, out, (size_t)r * cols + c, r, c);
+    return LLMI_OK;
+}
+
+}  // namespace llmi

@@ -1,0 +1,106 @@
+"""ctypes binding of libllmi.so (include/llmi.h).
+
+The shared library is the product: this module only declares signatures and
+turns negative return codes into exceptions. There is no fallback -- if the
+library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(_HERE)
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "lib", "libllmi.so")
+HEADER = os.path.join(REPO, "include", "llmi.h")
+
+F32, F16, I8, I32 = 0, 1, 2, 3
+SYN_LINEAR, SYN_EMBED, SYN_GAMMA, SYN_INT8, SYN_INT8_SCALE = 0, 1, 2, 3, 4
+
+
+class LlmiError(RuntimeError):
+    pass
+
+
+class Config(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("hidden", "heads", "kv_heads", "head_dim", "inter", "layers",
+                                        "vocab", "max_seq")] + \
+               [("rms_eps", C.c_float), ("rope_base", C.c_float)] + \
+               [(n, C.c_int) for n in ("weight_dtype", "kv_dtype", "tp_rank", "tp_world")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_P, _I, _U64, _U32, _F, _SZ = C.c_void_p, C.c_int, C.c_uint64, C.c_uint32, C.c_float, C.c_size_t
+_SIGS = {
+    "llmi_last_error": (C.c_char_p, []),
+    "llmi_version": (C.c_char_p, []),
+    "llmi_embedding": (_I, [_P, _I, _P, _I, _I, _I, _P, _P]),
+    "llmi_rmsnorm": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _P]),
+    "llmi_add_residual_rmsnorm": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _F, _P]),
+    "llmi_add_residual": (_I, [_P, _P, _I, _I, _P]),
+    "llmi_silu_mul": (_I, [_P, _P, _I, _I, _P]),
+    "llmi_linear": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _P]),
+    "llmi_rope_decode": (_I, [_P, _I, _I, _I, _I, _F, _P]),
+    "llmi_attn_workspace_bytes": (_SZ, [_I, _I, _I]),
+    "llmi_attn_decode": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P]),
+    "llmi_argmax": (_I, [_P, _I, _P, _P]),
+    "llmi_synth_fill": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I, _P]),
+    "llmi_synth_fill_host": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I]),
+    "llmi_synth_prompt": (_I, [_U64, _I, _I, _P]),
+    "llmi_config_preset": (_I, [C.c_char_p, C.POINTER(Config)]),
+    "llmi_tp_unique_id": (_I, [_P]),
+    "llmi_engine_create": (_I, [C.POINTER(Config), _I, _P, C.POINTER(_P)]),
+    "llmi_engine_destroy": (_I, [_P]),
+    "llmi_engine_load_synthetic": (_I, [_P, _U64]),
+    "llmi_engine_set_prompt": (_I, [_P, _P, _I]),
+    "llmi_engine_decode": (_I, [_P, _I, _I]),
+    "llmi_engine_sync": (_I, [_P]),
+    "llmi_engine_tokens": (_I, [_P, _P, _I, C.POINTER(_I)]),
+    "llmi_engine_logits": (_I, [_P, _P, _I]),
+    "llmi_engine_hidden": (_I, [_P, _P, _I]),
+    "llmi_engine_kv_slot": (_I, [_P, _I, _I, _I, _P]),
+    "llmi_engine_bytes": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64)]),
+    "llmi_engine_stream": (_P, [_P]),
+    "llmi_engine_time_kernel": (_I, [_P, _I, _I, C.POINTER(_F), C.POINTER(_U64)]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libllmi.so once. Raises if it has not been built -- no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libllmi.so not found at {LIB_PATH}; build it with "
+                              f"`python llm-inference_amd/build.py` (HIP extension is required)")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().llmi_last_error().decode(errors="replace")
+        raise LlmiError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    check(rc, name)
+    return rc
+
+
+def header_functions() -> list:
+    """Names of the functions include/llmi.h declares (for the export check)."""
+    import re
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(llmi_[a-z0-9_]+)\s*\(", src)))

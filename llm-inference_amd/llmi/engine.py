@@ -1,0 +1,123 @@
+"""Python handle on the native decode engine (llmi_engine_* in include/llmi.h).
+
+Mirrors the reference's model-level API (src/models/basemodel.h:14-42,
+src/utils/model_utils.h:63-70): build a Llama with dummy (here: synthetic
+PRNG) weights, feed a prompt, greedy-decode. All compute runs in
+libllmi.so on the GPU; this class only moves ids/logits across the boundary.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import F16, F32, I8, Config, call
+
+
+def preset(name: str, **overrides) -> Config:
+    cfg = Config()
+    call("llmi_config_preset", name.encode(), C.byref(cfg))
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def tp_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    call("llmi_tp_unique_id", buf)
+    return buf.raw
+
+
+def synth_prompt(seed: int, n: int, vocab: int) -> np.ndarray:
+    out = np.zeros(n, np.int32)
+    call("llmi_synth_prompt", seed, n, vocab, out.ctypes.data)
+    return out
+
+
+class Engine:
+    def __init__(self, cfg: Config, device: int = 0, tp_id: Optional[bytes] = None):
+        self.cfg = cfg
+        h = C.c_void_p()
+        idbuf = C.create_string_buffer(tp_id, 128) if tp_id else None
+        call("llmi_engine_create", C.byref(cfg), device, idbuf, C.byref(h))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().llmi_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------------ api
+    def load_synthetic(self, seed: int):
+        call("llmi_engine_load_synthetic", self._h, seed)
+
+    def set_prompt(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        call("llmi_engine_set_prompt", self._h, ids.ctypes.data, len(ids))
+
+    def decode(self, n_steps: int, use_graph: bool = True):
+        call("llmi_engine_decode", self._h, n_steps, 1 if use_graph else 0)
+
+    def sync(self):
+        call("llmi_engine_sync", self._h)
+
+    def tokens(self, n: Optional[int] = None) -> np.ndarray:
+        n = self.cfg.max_seq + 1 if n is None else n
+        out = np.zeros(n, np.int32)
+        valid = C.c_int()
+        call("llmi_engine_tokens", self._h, out.ctypes.data, n, C.byref(valid))
+        return out[:min(n, valid.value)]
+
+    def logits(self) -> np.ndarray:
+        n = self.cfg.vocab // self.cfg.tp_world
+        out = np.zeros(n, np.float32)
+        call("llmi_engine_logits", self._h, out.ctypes.data, n)
+        return out
+
+    def hidden(self) -> np.ndarray:
+        out = np.zeros(self.cfg.hidden, np.float32)
+        call("llmi_engine_hidden", self._h, out.ctypes.data, self.cfg.hidden)
+        return out
+
+    def kv_slot(self, layer: int, pos: int, which_v: bool = False) -> np.ndarray:
+        kvl = self.cfg.kv_heads // self.cfg.tp_world
+        out = np.zeros((kvl, self.cfg.head_dim), np.float32)
+        call("llmi_engine_kv_slot", self._h, layer, pos, 1 if which_v else 0, out.ctypes.data)
+        return out
+
+    def bytes_per_token(self):
+        w, kv = C.c_uint64(), C.c_uint64()
+        call("llmi_engine_bytes", self._h, C.byref(w), C.byref(kv))
+        return w.value, kv.value
+
+    def stream(self) -> int:
+        return _lib.lib().llmi_engine_stream(self._h) or 0
+
+    KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5}
+
+    def time_kernel(self, which: str, iters: int = 50):
+        us, b = C.c_float(), C.c_uint64()
+        call("llmi_engine_time_kernel", self._h, self.KERNELS[which], iters, C.byref(us), C.byref(b))
+        return us.value, b.value
+
+    def generate(self, prompt, n_new: int, use_graph: bool = True) -> np.ndarray:
+        """Greedy: feed the prompt, produce n_new tokens (Llama<T>::Response)."""
+        prompt = np.asarray(prompt, np.int32)
+        self.set_prompt(prompt)
+        self.decode(len(prompt) + n_new - 1, use_graph)
+        toks = self.tokens(len(prompt) + n_new)
+        return toks[len(prompt):]

@@ -1,0 +1,124 @@
+"""Operator API on torch device tensors -> libllmi.so kernels.
+
+One function per reference launcher on the decode path (src/kernels/*.h),
+same names and argument meaning, fp32 activations. torch is only the
+device-memory / stream plumbing here: every op launches the HIP kernel
+through the C ABI on torch's current stream and raises on a non-zero status.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import F16, F32, I8, call
+
+_DT = {torch.float32: F32, torch.float16: F16, torch.int8: I8}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dt(t):
+    return _DT[t.dtype]
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("llmi ops need device tensors")
+
+
+def launchInputEmbedding(input_ids: torch.Tensor, embed_table: torch.Tensor) -> torch.Tensor:
+    _dev(input_ids, embed_table)
+    ids = input_ids.to(torch.int32).contiguous().view(-1)
+    out = torch.empty(ids.numel(), embed_table.shape[1], device=ids.device, dtype=torch.float32)
+    call("llmi_embedding", ids.data_ptr(), ids.numel(), embed_table.data_ptr(), _dt(embed_table),
+         embed_table.shape[0], embed_table.shape[1], out.data_ptr(), _stream())
+    return out
+
+
+def launchRMSNorm(decoder_out: torch.Tensor, gamma: torch.Tensor, eps: float,
+                  decoder_residual: torch.Tensor = None) -> torch.Tensor:
+    """In place on decoder_out (the reference's convention); optionally saves pre-norm x."""
+    _dev(decoder_out, gamma)
+    n, h = decoder_out.shape
+    call("llmi_rmsnorm", decoder_out.data_ptr(), decoder_out.data_ptr(), _p(decoder_residual),
+         gamma.data_ptr(), _dt(gamma), n, h, float(eps), _stream())
+    return decoder_out
+
+
+def launchFusedAddBiasResidualRMSNorm(residual, decoder_out, gamma, eps, bias=None):
+    _dev(residual, decoder_out, gamma)
+    n, h = decoder_out.shape
+    call("llmi_add_residual_rmsnorm", residual.data_ptr(), decoder_out.data_ptr(), _p(bias),
+         _dt(bias) if bias is not None else F32, gamma.data_ptr(), _dt(gamma), n, h, float(eps), _stream())
+    return residual, decoder_out
+
+
+def launchAddResidual(residual, decoder_out):
+    _dev(residual, decoder_out)
+    n, h = decoder_out.shape
+    call("llmi_add_residual", residual.data_ptr(), decoder_out.data_ptr(), n, h, _stream())
+    return decoder_out
+
+
+def launchAct(gate_up: torch.Tensor) -> torch.Tensor:
+    """gate_up [n, 2, inter] -> silu(gate) * up [n, inter]."""
+    _dev(gate_up)
+    n, _, inter = gate_up.shape
+    out = torch.empty(n, inter, device=gate_up.device, dtype=torch.float32)
+    call("llmi_silu_mul", gate_up.data_ptr(), out.data_ptr(), n, inter, _stream())
+    return out
+
+
+def launchLinearGemm(x: torch.Tensor, w: torch.Tensor, scales: torch.Tensor = None) -> torch.Tensor:
+    """y = x @ w^T (trans_b = true); w [n, k] f32/f16/i8 (+ per-row f16 scales for i8)."""
+    _dev(x, w)
+    m, k = x.shape
+    n = w.shape[0]
+    y = torch.empty(m, n, device=x.device, dtype=torch.float32)
+    call("llmi_linear", x.data_ptr(), w.data_ptr(), _dt(w), _p(scales), y.data_ptr(), m, n, k, _stream())
+    return y
+
+
+def launchRoPE(qkv: torch.Tensor, pos: int, heads: int, kv_heads: int, head_dim: int = 128,
+               base: float = 10000.0) -> torch.Tensor:
+    _dev(qkv)
+    call("llmi_rope_decode", qkv.data_ptr(), int(pos), heads, kv_heads, head_dim, float(base), _stream())
+    return qkv
+
+
+def attn_workspace(heads: int, max_seq: int, head_dim: int = 128, device="cuda") -> torch.Tensor:
+    n = _lib.lib().llmi_attn_workspace_bytes(heads, head_dim, max_seq)
+    return torch.zeros(n, dtype=torch.uint8, device=device)
+
+
+def launchDecoderMaskedMHA(qkv, k_cache, v_cache, layer: int, pos: int, heads: int, kv_heads: int,
+                           workspace, rope: bool = False, base: float = 10000.0, head_dim: int = 128):
+    """k_cache/v_cache [layers, kv_heads, max_seq, d] f16/f32; returns out [heads * d] fp32."""
+    _dev(qkv, k_cache, v_cache, workspace)
+    max_seq = k_cache.shape[2]
+    out = torch.empty(heads * head_dim, device=qkv.device, dtype=torch.float32)
+    call("llmi_attn_decode", qkv.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), _dt(k_cache), layer,
+         max_seq, int(pos), heads, kv_heads, head_dim, 1 if rope else 0, float(base), out.data_ptr(),
+         workspace.data_ptr(), _stream())
+    return out
+
+
+def argmax(logits: torch.Tensor) -> torch.Tensor:
+    _dev(logits)
+    out = torch.empty(1, device=logits.device, dtype=torch.int32)
+    call("llmi_argmax", logits.data_ptr(), logits.numel(), out.data_ptr(), _stream())
+    return out
+
+
+def synth_fill(out: torch.Tensor, kind: int, seed: int, tid: int, rows: int, cols: int,
+               row0: int = 0, col0: int = 0, ld: int = 0) -> torch.Tensor:
+    _dev(out)
+    call("llmi_synth_fill", out.data_ptr(), _dt(out), kind, seed, tid, rows, cols, row0, col0, ld, _stream())
+    return out

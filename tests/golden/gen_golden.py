@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures by running the REFERENCE's own modeling_llama.py.
+
+Runs only in the build container (where /root/reference exists); the GPU box
+never executes this file. It imports /root/reference/modeling_llama.py in
+memory with the three shims of SURVEY.md Appendix B (the file targets
+transformers ~4.36; this image has transformers 5.x), fills the reference
+modules with the portable PRNG weights of oracle/prng.py (fp16 values held
+as fp32, i.e. the reference's fp32 CPU path), and records inputs + outputs:
+
+  f1_ops.npz      per-op vectors at 7B width: RMSNorm, RoPE at positions
+                  {0,1,127,128,2047}, SiLU*mul (LlamaMLP act), q_proj rows
+  f2_layer.npz    config 1: one LlamaDecoderLayer, hidden 4096, seq 8, fp32
+  f3_decode.npz   2-layer 7B-width model: 8-token prompt, 16 greedy steps,
+                  token ids, logits of the first and last step, layer-0 K/V
+  f4_tp8.npz      f3 with pretraining_tp = 8 (sharded-linear semantics)
+  f5_int8.npz     13B-width 1-layer W8A16 model (dequantised weights)
+  f6_prefill.npz  7B-width 1 layer, prefill seq 512, last-token logits
+  tiny.npz        test_llama_run.py-like tiny model (hidden 512, 2 layers)
+  manifest.json   versions + what each fixture holds
+
+Weights are NOT stored (they are regenerated from the seed); only ids,
+activations and outputs are. Usage: python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+from oracle import prng  # noqa: E402
+from oracle.llama_ref import LlamaConfig, make_model_weights  # noqa: E402
+
+REF = "/root/reference/modeling_llama.py"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def load_reference():
+    """SURVEY.md Appendix B recipe: our harness code around the reference file."""
+    import transformers.utils.import_utils as iu
+    iu.is_torch_fx_available = getattr(iu, "is_torch_fx_available", lambda: False)
+    import transformers.models.llama  # noqa: F401  parent package for relative imports
+    name = "transformers.models.llama.ref_modeling_llama"
+    spec = importlib.util.spec_from_file_location(name, REF)
+    ref = importlib.util.module_from_spec(spec)
+    sys.modules[name] = ref
+    spec.loader.exec_module(ref)
+
+    class KV:  # stands in for the v4.36 DynamicCache API (modeling_llama.py:402,408,1016-1017)
+        def __init__(s):
+            s.k, s.v = [], []
+
+        def get_usable_length(s, n, i=0):
+            return s.k[i].shape[-2] if i < len(s.k) else 0
+
+        def update(s, k, v, i, kw=None):
+            if i == len(s.k):
+                s.k.append(k)
+                s.v.append(v)
+            else:
+                s.k[i] = torch.cat([s.k[i], k], -2)
+                s.v[i] = torch.cat([s.v[i], v], -2)
+            return s.k[i], s.v[i]
+
+    ref.Cache = KV
+    return ref, KV
+
+
+def ref_config(ref, c: LlamaConfig, tp: int = 1):
+    cfg = ref.LlamaConfig(hidden_size=c.hidden, intermediate_size=c.inter,
+                          num_hidden_layers=c.layers, num_attention_heads=c.heads,
+                          num_key_value_heads=c.kv_heads, vocab_size=c.vocab,
+                          rms_norm_eps=c.rms_eps, max_position_embeddings=max(c.max_seq, 2048))
+    for k, v in dict(_attn_implementation="eager", rope_theta=c.rope_base, rope_scaling=None,
+                     pretraining_tp=tp, attention_bias=False, attention_dropout=0.0,
+                     hidden_act="silu").items():
+        object.__setattr__(cfg, k, v)
+    return cfg
+
+
+def f32(a):
+    return torch.from_numpy(np.ascontiguousarray(a.astype(np.float32)))
+
+
+def build_model(ref, c: LlamaConfig, seed: int, tp: int = 1, int8: bool = False):
+    torch.manual_seed(0)
+    m = ref.LlamaForCausalLM(ref_config(ref, c, tp)).eval()
+    w = make_model_weights(c, seed, int8=int8)
+    from oracle.llama_ref import dequant
+    sd = {"model.embed_tokens.weight": f32(w.embed), "lm_head.weight": f32(w.lm_head),
+          "model.norm.weight": f32(w.final_norm)}
+    q, kv, I = c.q_rows, c.kv_rows, c.inter
+    for l, lw in enumerate(w.layers):
+        p = f"model.layers.{l}."
+        qkv = dequant(lw.qkv, lw.qkv_s)
+        gu = dequant(lw.gate_up, lw.gate_up_s)
+        sd[p + "self_attn.q_proj.weight"] = f32(qkv[:q])
+        sd[p + "self_attn.k_proj.weight"] = f32(qkv[q:q + kv])
+        sd[p + "self_attn.v_proj.weight"] = f32(qkv[q + kv:])
+        sd[p + "self_attn.o_proj.weight"] = f32(dequant(lw.o, lw.o_s))
+        sd[p + "mlp.gate_proj.weight"] = f32(gu[:I])
+        sd[p + "mlp.up_proj.weight"] = f32(gu[I:])
+        sd[p + "mlp.down_proj.weight"] = f32(dequant(lw.down, lw.down_s))
+        sd[p + "input_layernorm.weight"] = f32(lw.attn_norm)
+        sd[p + "post_attention_layernorm.weight"] = f32(lw.ffn_norm)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if "rotary_emb" not in k]
+    assert not missing and not unexpected, (missing, unexpected)
+    return m
+
+
+@torch.no_grad()
+def greedy_ref(ref, KV, m, prompt: np.ndarray, n_new: int, keep_kv_pos=()):
+    cache = KV()
+    ids = torch.from_numpy(prompt.astype(np.int64))[None]
+    out = m(input_ids=ids, past_key_values=cache, use_cache=True)
+    logits = out.logits[0, -1].float().numpy()
+    first_logits = logits.copy()
+    toks, pos = [], len(prompt)
+    for i in range(n_new):
+        t = int(np.argmax(logits))
+        toks.append(t)
+        if i + 1 == n_new:
+            break
+        out = m(input_ids=torch.tensor([[t]]), position_ids=torch.tensor([[pos]]),
+                past_key_values=cache, use_cache=True)
+        logits = out.logits[0, -1].float().numpy()
+        pos += 1
+    kv = {}
+    for p in keep_kv_pos:
+        kv[f"k_l0_p{p}"] = cache.k[0][0, :, p].numpy().astype(np.float32)
+        kv[f"v_l0_p{p}"] = cache.v[0][0, :, p].numpy().astype(np.float32)
+    return np.array(toks, np.int32), first_logits, logits, kv
+
+
+@torch.no_grad()
+def gen_f1(ref, seed=11):
+    c = LlamaConfig(layers=1)
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((4, c.hidden)).astype(np.float32)
+    gamma = prng.gamma_fp16(seed, prng.layer_tid(0, prng.KIND_ATTN_NORM), c.hidden)
+    norm = ref.LlamaRMSNorm(c.hidden, eps=c.rms_eps)
+    norm.weight.data = f32(gamma)
+    rms_out = norm(f32(x)).numpy()
+    # RoPE on q/k [1, heads, npos, d] at chosen positions
+    positions = np.array([0, 1, 127, 128, 2047], np.int64)
+    q = rng.standard_normal((1, c.heads, len(positions), c.head_dim)).astype(np.float32)
+    k = rng.standard_normal((1, c.kv_heads, len(positions), c.head_dim)).astype(np.float32)
+    rot = ref.LlamaRotaryEmbedding(c.head_dim, max_position_embeddings=2048, base=c.rope_base)
+    cos, sin = rot(f32(q), seq_len=2048)
+    qe, ke = ref.apply_rotary_pos_emb(f32(q), f32(k), cos, sin, torch.from_numpy(positions)[None])
+    # SiLU*mul exactly as LlamaMLP forms it (modeling_llama.py:268)
+    gu = rng.standard_normal((2, 3 * 512)).astype(np.float32) * 3
+    act = ref.ACT2FN["silu"]
+    silu_mul = (act(f32(gu[:, :512 * 1])) * f32(gu[:, 512:1024])).numpy()
+    # q_proj rows 0..255 of layer 0 (fp16 weights as fp32) applied to x
+    wq = prng.linear_fp16(seed, prng.layer_tid(0, prng.KIND_Q), 256, c.hidden)
+    lin = torch.nn.functional.linear(f32(x), f32(wq)).numpy()
+    np.savez_compressed(os.path.join(OUT, "f1_ops.npz"), seed=seed, x=x, rms_out=rms_out,
+                        rope_pos=positions, rope_q=q, rope_k=k, rope_q_out=qe.numpy(),
+                        rope_k_out=ke.numpy(), silu_in=gu[:, :1024], silu_mul_out=silu_mul,
+                        linear_out=lin)
+
+
+@torch.no_grad()
+def gen_f2(ref, seed=12):
+    """Config 1: one decoder layer forward, hidden 4096, seq 8, fp32 (BASELINE.json configs[0])."""
+    c = LlamaConfig(layers=1)
+    m = build_model(ref, c, seed)
+    layer = m.model.layers[0]
+    x = np.random.default_rng(seed).standard_normal((1, 8, c.hidden)).astype(np.float32)
+    mask = torch.full((8, 8), float("-inf")).triu(1)[None, None]
+    pos = torch.arange(8)[None]
+    kw = {}
+    if hasattr(m.model, "rotary_emb"):
+        kw["position_embeddings"] = m.model.rotary_emb(f32(x), pos)
+    t0 = time.perf_counter()
+    y = layer(f32(x), attention_mask=mask, position_ids=pos, **kw)[0].numpy()
+    dt = time.perf_counter() - t0
+    np.savez_compressed(os.path.join(OUT, "f2_layer.npz"), seed=seed, x=x, y=y, ref_cpu_s=dt)
+
+
+def gen_decode(ref, KV, c, seed, tp, fname, n_new=16, int8=False, keep_kv_pos=(0, 7, 22)):
+    m = build_model(ref, c, seed, tp=tp, int8=int8)
+    prompt = prng.prompt_ids(seed, 8, c.vocab)
+    t0 = time.perf_counter()
+    toks, first, last, kv = greedy_ref(ref, KV, m, prompt, n_new, keep_kv_pos)
+    dt = time.perf_counter() - t0
+    np.savez_compressed(os.path.join(OUT, fname), seed=seed, prompt=prompt, tokens=toks,
+                        first_logits=first, last_logits=last, ref_cpu_s=dt, **kv)
+    return toks
+
+
+@torch.no_grad()
+def gen_f6(ref, seed=16, seq=512):
+    c = LlamaConfig(layers=1)
+    m = build_model(ref, c, seed)
+    ids = prng.prompt_ids(seed + 1, seq, c.vocab)
+    out = m(input_ids=torch.from_numpy(ids.astype(np.int64))[None], use_cache=False)
+    np.savez_compressed(os.path.join(OUT, "f6_prefill.npz"), seed=seed, ids=ids,
+                        last_logits=out.logits[0, -1].float().numpy(),
+                        logits_rows=out.logits[0, [0, 1, 255, 511]].float().numpy())
+
+
+def main():
+    ref, KV = load_reference()
+    torch.set_num_threads(os.cpu_count() or 8)
+    import transformers
+    manifest = {"torch": torch.__version__, "transformers": transformers.__version__,
+                "numpy": np.__version__, "reference": REF, "prng": "llmi-prng-v1 (oracle/prng.py)",
+                "fixtures": {}}
+    steps = [
+        ("f1_ops.npz", lambda: gen_f1(ref)),
+        ("f2_layer.npz", lambda: gen_f2(ref)),
+        ("tiny.npz", lambda: gen_decode(ref, KV, LlamaConfig(hidden=512, heads=4, kv_heads=4,
+                                                              inter=1024, layers=2, vocab=32000,
+                                                              max_seq=64), 21, 1, "tiny.npz", n_new=24)),
+        ("f3_decode.npz", lambda: gen_decode(ref, KV, LlamaConfig(layers=2), 13, 1, "f3_decode.npz")),
+        ("f4_tp8.npz", lambda: gen_decode(ref, KV, LlamaConfig(layers=2), 13, 8, "f4_tp8.npz")),
+        ("f5_int8.npz", lambda: gen_decode(ref, KV, LlamaConfig(hidden=5120, heads=40, kv_heads=40,
+                                                                 inter=13824, layers=1), 15, 1,
+                                            "f5_int8.npz", n_new=8, int8=True,
+                                            keep_kv_pos=(0, 7, 14))),
+        ("f6_prefill.npz", lambda: gen_f6(ref)),
+    ]
+    only = set(sys.argv[1:])
+    for name, fn in steps:
+        if only and name not in only:
+            continue
+        t0 = time.time()
+        fn()
+        print(f"{name}: {time.time() - t0:.1f}s", flush=True)
+        manifest["fixtures"][name] = {"generated_s": round(time.time() - t0, 1)}
+    mpath = os.path.join(OUT, "manifest.json")
+    if os.path.exists(mpath) and only:
+        old = json.load(open(mpath))
+        old["fixtures"].update(manifest["fixtures"])
+        manifest["fixtures"] = old["fixtures"]
+    json.dump(manifest, open(mpath, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
