@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Decode benchmark: Llama-2-7B fp16 single-stream greedy decode to 2048 tokens.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+One "step" = one full greedy generation on the BASELINE.json configs[1]
+workload: synthetic random-init Llama-2-7B weights (llmi-prng-v1, fp16), an
+8-token synthetic prompt, then single-token decode forwards at positions
+0..2047 (ctx 1..2048; 2048 forwards, 2041 generated tokens), all inside the
+native engine (one hipGraph replay per token). N > 1 runs tensor parallel over
+N GPUs (config 4: head/FFN row/col shard + RCCL all-reduce); each rank streams
+1/N of the weights, total work is fixed ("strong" scaling).
+
+value = generated tokens / s (whole job). Also reported: HBM roofline of the
+dominant kernel (gate_up GEMV, HIP events on the engine stream), the whole
+decode loop's algorithmic HBM fraction, and a CPU baseline (the numpy oracle,
+rank 0 at N = 1 only, bounded sample, scaled to the same unit).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "llm-inference_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+MAX_SEQ = 2048
+PROMPT = 8
+SEED = 0
+
+
+def algorithmic_bytes(weight_bytes: int, kv_per_pos: int, n_fwd: int) -> int:
+    """Sum over forwards at ctx = 1..n_fwd of weights + KV read (ctx slots) + KV write (1 slot)."""
+    ctx_sum = n_fwd * (n_fwd + 1) // 2
+    return n_fwd * weight_bytes + kv_per_pos * (ctx_sum + n_fwd)
+
+
+def cpu_baseline(sample_layers: int = 2, n_fwd: int = 48):
+    """Oracle (numpy, fp32) timed on this host: 7B width, `sample_layers` layers +
+    lm_head, n_fwd decode forwards at ctx 1..n_fwd; scaled to 32 layers."""
+    from threadpoolctl import threadpool_info
+
+    from oracle import llama_ref as R
+    from oracle import prng
+    cfg = R.LlamaConfig(layers=sample_layers, max_seq=n_fwd + 1)
+    o = R.LlamaOracle(cfg, seed=SEED)
+    ids = prng.prompt_ids(SEED, PROMPT, cfg.vocab)
+    t0 = time.perf_counter()
+    logits = None
+    for i in range(n_fwd):
+        tok = int(ids[i]) if i < PROMPT else int(np.argmax(logits))
+        logits = o.forward_token(tok)
+    t_fwd = (time.perf_counter() - t0) / n_fwd
+    x = o.last_hidden
+    t0 = time.perf_counter()
+    for _ in range(n_fwd):
+        R.linear(R.rmsnorm(x, o.final_norm, cfg.rms_eps), o.lm_head)
+    t_head = (time.perf_counter() - t0) / n_fwd
+    t_layer = (t_fwd - t_head) / sample_layers
+    per_tok = t_head + 32 * t_layer
+    threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    return {"value": round(1.0 / per_tok, 4), "unit": "tokens/s", "cores": int(threads), "kind": "port",
+            "sample": f"numpy oracle (oracle/llama_ref.py, fp32), Llama-2-7B width, {sample_layers} layers + "
+                      f"lm_head, {n_fwd} greedy decode forwards at ctx 1..{n_fwd}; per-token time = lm_head + "
+                      f"32 x measured per-layer time ({t_layer * 1e3:.1f} ms/layer, {t_head * 1e3:.1f} ms head)"}
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc pass (profiles/), if present."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        return d["kernels"][kernel]["hbm_bytes_per_launch"], d.get("source")
+    except Exception:
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--max-seq", type=int, default=MAX_SEQ)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kv", choices=["f16", "f32"], default="f16")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch kernels eagerly instead of replaying the hipGraph (profiling: rocprofv3 "
+                         "kernel tracing of graph replays crashes on ROCm 7.2)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import llmi
+    from llmi.engine import Engine, preset, synth_prompt, tp_unique_id
+
+    dist = None
+    tp_id = None
+    if world > 1:
+        import torch.distributed as dist  # plumbing only: id exchange, barrier, max
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        obj = [tp_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        tp_id = obj[0]
+
+    cfg = preset("llama2-7b", max_seq=args.max_seq, tp_rank=rank, tp_world=world)
+    cfg.kv_dtype = llmi.F16 if args.kv == "f16" else llmi.F32
+    eng = Engine(cfg, device=local, tp_id=tp_id)
+    eng.load_synthetic(SEED)
+    prompt = synth_prompt(SEED, PROMPT, cfg.vocab)
+    n_fwd = cfg.max_seq
+    gen_per_step = n_fwd - PROMPT + 1
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def one_generation():
+        eng.set_prompt(prompt)
+        eng.decode(n_fwd, use_graph=not args.eager)
+
+    for _ in range(args.warmup):
+        one_generation()
+    eng.sync()
+    barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_generation()
+    eng.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    toks = eng.tokens(n_fwd + 1)
+    consistent = True
+    if dist is not None:
+        objs = [None] * world
+        dist.all_gather_object(objs, toks[:64].tolist())
+        consistent = all(o == objs[0] for o in objs)
+
+    wbytes, kvb = eng.bytes_per_token()
+    # dominant kernel: gate_up GEMV of layer 0, timed with HIP events on the engine stream
+    gu_us, gu_bytes = eng.time_kernel("gate_up", iters=200)
+    kern = {k: eng.time_kernel(k, iters=100) for k in ("qkv", "attn", "o", "down", "lm_head")}
+    eng.close()
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+    value = gen_per_step * args.steps / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+    per_rank_bytes = algorithmic_bytes(wbytes, kvb, n_fwd)
+    traffic, traffic_src = pmc_traffic("gate_up")
+    achieved = gu_bytes / (gu_us * 1e-6) / 1e9
+    out = {
+        "metric": "decode tokens/sec Llama-2-7B fp16 @1 GPU; % HBM roofline; 1->8 TP curve",
+        "value": round(value, 2),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp16",
+        "data": "synthetic (llmi-prng-v1 random-init Llama-2-7B weights, 8 PRNG prompt ids)",
+        "config": {"workload": "Llama-2-7B fp16 single-stream greedy decode to 2048 tokens "
+                               "(BASELINE.json configs[1]); TP over n_gpus when > 1",
+                   "batch": 1, "prompt": PROMPT, "ctx": f"1..{n_fwd}", "forwards_per_step": n_fwd,
+                   "generated_per_step": gen_per_step, "kv_cache": args.kv,
+                   "weights": "fp16, fp32 activations/accumulate",
+                   "parallelism": f"tp{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": "gate_up GEMV (rmsnorm+gate_up+silu*mul), layer 0",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes": gu_bytes, "avg_us": round(gu_us, 2),
+                     "traffic_source": traffic_src},
+        "decode_loop_hbm": {"bytes_per_step_per_rank": per_rank_bytes,
+                            "achieved_GBps_per_rank": round(per_rank_bytes / (elapsed / args.steps) / 1e9, 1),
+                            "frac_of_8TBps": round(per_rank_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                            "weight_bytes_per_token": wbytes, "kv_bytes_per_pos": kvb},
+        "kernels_us": {"gate_up": round(gu_us, 2), **{k: round(v[0], 2) for k, v in kern.items()}},
+        "kernels_GBps": {"gate_up": round(achieved, 1),
+                         **{k: round(v[1] / (v[0] * 1e-6) / 1e9, 1) for k, v in kern.items()}},
+        "tp_tokens_consistent": consistent,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline()
+        except Exception as e:  # reported, never fatal to the GPU number
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,13 +19,14 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(HERE, "build")
+_TAG = os.environ.get("LLMI_BUILD_TAG", "")  # tuning variants: build_<tag>/, lib/libllmi_<tag>.so
+BUILD = os.path.join(HERE, "build" + (f"_{_TAG}" if _TAG else ""))
 LIBDIR = os.path.join(HERE, "lib")
-LIB = os.path.join(LIBDIR, "libllmi.so")
+LIB = os.path.join(LIBDIR, f"libllmi_{_TAG}.so" if _TAG else "libllmi.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("LLMI_ARCH", "gfx950")
 
-CFLAGS = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+CFLAGS = [*os.environ.get("LLMI_EXTRA_CFLAGS", "").split(), "-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-I" + os.path.join(REPO, "include"), "-I" + CSRC, "-D__HIP_PLATFORM_AMD__"]
 LDFLAGS = ["-shared", f"--offload-arch={ARCH}", "-L/opt/rocm/lib", "-lrccl", "-lamdhip64",
            "-Wl,-rpath,/opt/rocm/lib"]

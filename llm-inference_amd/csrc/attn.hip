@@ -1,26 +1,30 @@
-// Fused decode attention for one token: RoPE(q, k) + KV-cache write + split-KV
-// softmax(q K^T / sqrt(d)) V with a log-sum-exp merge by the last-arriving
-// workgroup of each head.
+// Decode attention for one token: RoPE(q, k) + KV-cache write + split-KV
+// softmax(q K^T / sqrt(d)) V, and the two consumers of its split partials:
+//   * attn_merge_kernel: log-sum-exp merge -> out[heads * d] (operator API);
+//   * attn_oproj_kernel: merge fused into a split-by-head O projection whose
+//     per-head partial products are summed into the residual stream with
+//     int64 fixed-point atomics (engine path; exact, order-independent sums).
 //
-// Replaces launchRoPE + launchDecoderMaskedMHA (src/kernels/qkv_bias_and_RoPE.cu:322-451,
-// src/kernels/fused_decoder_self_attention.cu:97-385; layer call sites
-// src/layers/attention/masked_self_attention.cpp:76-80). Semantics follow
-// modeling_llama.py:351-437 (HF eager attention, fp32 softmax, no +1e-6 in the
+// Replaces launchRoPE + launchDecoderMaskedMHA (+ the o_proj launchLinearGemm)
+// (src/kernels/qkv_bias_and_RoPE.cu:322-451, src/kernels/fused_decoder_self_attention.cu:97-385,
+// src/layers/attention/masked_self_attention.cpp:76-84). Semantics follow
+// modeling_llama.py:351-448 (HF eager attention, fp32 softmax, no +1e-6 in the
 // denominator); none of the reference kernel's defects (SURVEY App. A #1-#6:
 // kv-head 0 for every head, missing kv_head in the layer offset, softmax capped at
 // 128 positions, empty fp16 path) are carried over.
 //
-// Roofline: HBM. Algorithmic bytes per launch = 2 * ctx * kv_heads * d * sizeof(cache)
-// (K and V read) + 2 * kv_heads * d * sizeof(cache) (current slot write).
+// Roofline: HBM. Algorithmic bytes = 2 * ctx * kv_heads * d * sizeof(cache) (K and V
+// read) + 2 * kv_heads * d * sizeof(cache) (current slot write); attn_oproj adds
+// hidden * heads * d * sizeof(W) (the o_proj weights).
 //
 // Work split (MI355X): grid (heads, max_seq / 64). A workgroup (256 threads = 16
 // groups of 16 lanes) owns 64 cached positions of one head; a 16-lane group reads a
-// 256-byte fp16 K/V row with one 16-B load per lane (4 rows per wave instruction).
-// 32 heads alone would use 32 of 256 CUs; at ctx 2048 the split gives 1024
-// workgroups. Partial (m, l, o) go to a workspace; an agent-scope release +
-// relaxed ticket per head selects the last arriver, which acquires and merges
-// (cdna_hip_programming.md §6 Guideline 16, split-K recipe). The counters are left
-// at zero for the next launch.
+// 256-byte fp16 K/V row with one 16-B load per lane (4 rows per wave instruction),
+// all its rows issued before anything waits. 32 heads alone would use 32 of 256 CUs;
+// at ctx 2048 the split gives 1024 workgroups. Each writes (m, l, o) partials; the
+// next kernel merges them (a kernel boundary orders the hand-off -- an in-kernel
+// last-arriver merge measured no faster: its store-drain + ticket + load chain costs
+// as much as the boundary, profiles/).
 #include "kernels.h"
 
 namespace llmi {
@@ -28,12 +32,44 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int D = 128;         // head_dim
-constexpr int CH = kAttnChunk;  // positions per workgroup
+#ifndef LLMI_ATTN_CH
+#define LLMI_ATTN_CH 64
+#endif
+constexpr int CH = LLMI_ATTN_CH;  // positions per workgroup (<= kAttnChunk sizes the workspace)
+static_assert(CH % 64 == 0 && CH >= kAttnChunk, "chunk must be a multiple of 64");
 constexpr int LPR = 16;        // lanes per cached row (8 dims per lane)
 
-__device__ __forceinline__ void load8(const __half* p, float* v) {
-    uint4 u = *reinterpret_cast<const uint4*>(p);
-    const __half2* h = reinterpret_cast<const __half2*>(&u);
+constexpr int NPG = CH / (kThreads / LPR);  // cached rows per 16-lane group
+constexpr int kMaxSplits = 1024;            // max_seq <= 64 Ki positions
+constexpr int kMergeChunk = 16;             // o-partials per thread in the first merge round
+static_assert(kThreads == 2 * D, "merge maps two threads to each head dim");
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_max(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float t = -INFINITY;
+    for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+    return t;
+}
+
+// 8 cache elements of one row, as loaded (16 B for fp16, 32 B for fp32)
+template <typename KT> struct Raw { uint4 v[sizeof(KT) / 2]; };
+__device__ __forceinline__ Raw<__half> ld_raw(const __half* p) {
+    Raw<__half> r;
+    r.v[0] = *reinterpret_cast<const uint4*>(p);
+    return r;
+}
+__device__ __forceinline__ Raw<float> ld_raw(const float* p) {
+    Raw<float> r;
+    r.v[0] = reinterpret_cast<const uint4*>(p)[0];
+    r.v[1] = reinterpret_cast<const uint4*>(p)[1];
+    return r;
+}
+__device__ __forceinline__ void unpack8(const Raw<__half>& r, float* v) {
+    const __half2* h = reinterpret_cast<const __half2*>(&r.v[0]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         float2 f = __half22float2(h[i]);
@@ -41,10 +77,14 @@ __device__ __forceinline__ void load8(const __half* p, float* v) {
         v[2 * i + 1] = f.y;
     }
 }
-__device__ __forceinline__ void load8(const float* p, float* v) {
-    float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+__device__ __forceinline__ void unpack8(const Raw<float>& r, float* v) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        v[4 * i + 0] = __uint_as_float(r.v[i].x);
+        v[4 * i + 1] = __uint_as_float(r.v[i].y);
+        v[4 * i + 2] = __uint_as_float(r.v[i].z);
+        v[4 * i + 3] = __uint_as_float(r.v[i].w);
+    }
 }
 __device__ __forceinline__ void store_cache(__half* p, float v) { *p = __float2half(v); }
 __device__ __forceinline__ void store_cache(float* p, float v) { *p = v; }
@@ -96,7 +136,6 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
     __shared__ float p_s[CH];
     __shared__ __attribute__((aligned(16))) float o_red[kThreads / LPR][D];  // [groups][D]
     __shared__ float ml_s[2];
-    __shared__ int last_s;
 
     const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
     if (pos < 0 || pos >= a.max_seq) return;  // host validates; guard against a stale state
@@ -111,6 +150,22 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
     const int kvh = h / group;
     const int tid = threadIdx.x;
     const bool owns_pos = (end == ctx);
+    const int grp = tid / LPR, l16 = tid % LPR;  // 16 groups x 16 lanes, 8 dims per lane
+
+    // ---- issue every K and V row load of this block first: they do not depend on
+    // q, so their HBM latency overlaps the q/RoPE prologue (NPG rows per lane each)
+    KT* kc = reinterpret_cast<KT*>(a.k_cache) + (size_t)kvh * a.max_seq * D;
+    KT* vc = reinterpret_cast<KT*>(a.v_cache) + (size_t)kvh * a.max_seq * D;
+    // branch-free: rows past `end` or at `pos` load a valid row (start) and are ignored
+    // later -- a predicated load would serialise the stream on vmcnt(0) waits
+    Raw<KT> kr[NPG], vr[NPG];
+#pragma unroll
+    for (int t = 0; t < NPG; ++t) {
+        const int j = start + grp + t * (kThreads / LPR);
+        const int jj = (j < end && j != pos) ? j : start;
+        kr[t] = ld_raw(kc + (size_t)jj * D + l16 * 8);
+        vr[t] = ld_raw(vc + (size_t)jj * D + l16 * 8);
+    }
 
     // ---- q (and the current k, v when this block owns position `pos`)
     const float* qrow = a.qkv + (size_t)h * D;
@@ -120,7 +175,13 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
     if (tid < D / 2) {
         const int i = tid;
         float c = 1.f, s = 0.f;
-        if (a.rope) rope_cs(pos, i, D, a.rope_base, &c, &s);
+        if (a.rope_tab) {
+            const float2 cs = reinterpret_cast<const float2*>(a.rope_tab)[(size_t)pos * (D / 2) + i];
+            c = cs.x;
+            s = cs.y;
+        } else if (a.rope) {
+            rope_cs(pos, i, D, a.rope_base, &c, &s);
+        }
         // rotate_half pairing (i, i + d/2): modeling_llama.py:204-235
         const float q0 = qrow[i], q1 = qrow[i + D / 2];
         q_s[i] = (q0 * c - q1 * s) * qscale;
@@ -135,8 +196,6 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
     }
     __syncthreads();
 
-    KT* kc = reinterpret_cast<KT*>(a.k_cache) + (size_t)kvh * a.max_seq * D;
-    KT* vc = reinterpret_cast<KT*>(a.v_cache) + (size_t)kvh * a.max_seq * D;
     if (owns_pos && (h % group) == 0 && tid < D) {
         // KV-cache write at slot pos (concat: fused_decoder_self_attention.cu:187-193,292-295)
         store_cache(kc + (size_t)pos * D + tid, kcur_s[tid]);
@@ -145,26 +204,27 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
     // The current position is always taken from LDS, never re-read from the cache,
     // so no other workgroup depends on the store above within this launch.
 
-    const int grp = tid / LPR, l16 = tid % LPR;  // 16 groups x 16 lanes
     float qv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) qv[i] = q_s[l16 * 8 + i];
 
     // ---- scores
-    for (int j = start + grp; j < end; j += kThreads / LPR) {
+#pragma unroll
+    for (int t = 0; t < NPG; ++t) {
+        const int j = start + grp + t * (kThreads / LPR);
         float kv[8];
         if (j == pos) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) kv[i] = kcur_s[l16 * 8 + i];
         } else {
-            load8(kc + (size_t)j * D + l16 * 8, kv);
+            unpack8(kr[t], kv);
         }
         float d = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) d = fmaf(qv[i], kv[i], d);
 #pragma unroll
         for (int off = LPR / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, kWave);
-        if (l16 == 0) p_s[j - start] = d;
+        if (l16 == 0 && j < end) p_s[j - start] = d;
     }
     __syncthreads();
 
@@ -184,13 +244,16 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
     float acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-    for (int j = start + grp; j < end; j += kThreads / LPR) {
+#pragma unroll
+    for (int t = 0; t < NPG; ++t) {
+        const int j = start + grp + t * (kThreads / LPR);
+        if (j >= end) break;
         float vv[8];
         if (j == pos) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) vv[i] = vcur_s[l16 * 8 + i];
         } else {
-            load8(vc + (size_t)j * D + l16 * 8, vv);
+            unpack8(vr[t], vv);
         }
         const float p = p_s[j - start];
 #pragma unroll
@@ -205,45 +268,218 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
 #pragma unroll
         for (int g = 0; g < kThreads / LPR; ++g) o += o_red[g][tid];
     }
-    if (nact == 1) {
+    if (a.direct_out && nact == 1) {  // operator API, one split: no merge needed
         if (tid < D) a.out[(size_t)h * D + tid] = o / ml_s[1];
         return;
     }
-
-    // ---- publish partial, last arriver merges
     Ws ws = ws_carve(a.workspace, a.heads, ns);
     if (tid < D) ws.o[((size_t)h * ns + split) * D + tid] = o;
     if (tid == 0) {
         ws.ml[((size_t)h * ns + split) * 2 + 0] = ml_s[0];
         ws.ml[((size_t)h * ns + split) * 2 + 1] = ml_s[1];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prev = __hip_atomic_fetch_add(ws.counters + h, 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        last_s = (prev == (unsigned)(nact - 1));
-        if (last_s) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+    // engine path: split 0 of head h seeds the fixed-point residual accumulator of
+    // the next kernel (attn_oproj) with its 128-element slice: fixed(resid) on the
+    // rank that carries the residual (TP rank 0), zero elsewhere
+    if (a.xacc != nullptr && split == 0) {
+        const int per = (a.hidden + a.heads - 1) / a.heads;
+        for (int i = h * per + tid; i < min((h + 1) * per, a.hidden); i += kThreads)
+            a.xacc[i] = a.resid_scale != 0.f ? to_fixed(a.resid[i]) : 0ll;
     }
+}
+
+// Log-sum-exp merge of the split-KV partials of each head (one workgroup per
+// head, 2 threads per head dim). Every load it needs -- the position, (m, l) of
+// every split and up to 2 * kMergeChunk o-partials per dim -- is issued in one
+// round; splits past nact hold stale data and are excluded by selects, never by
+// multiplying with a zero weight (stale NaN * 0 = NaN).
+__global__ __launch_bounds__(kThreads) void attn_merge_kernel(AttnArgs a, int ns) {
+    __shared__ float m_s[kMaxSplits];
+    __shared__ float l_s[kMaxSplits];
+    __shared__ float red_s[16];
+    __shared__ float o_red[2][D];
+    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
+    const int h = blockIdx.x, tid = threadIdx.x;
+    const int d = tid % D, half = tid / D;
+    Ws ws = ws_carve(a.workspace, a.heads, ns);
+    const float* mlh = ws.ml + (size_t)h * ns * 2;
+    const float* oh = ws.o + (size_t)h * ns * D + d;
+    float ov[kMergeChunk];
+#pragma unroll
+    for (int i = 0; i < kMergeChunk; ++i) {
+        const int sp = half + 2 * i;
+        ov[i] = oh[(size_t)(sp < ns ? sp : 0) * D];
+    }
+    for (int sp = tid; sp < ns; sp += kThreads) {
+        m_s[sp] = mlh[2 * sp];
+        l_s[sp] = mlh[2 * sp + 1];
+    }
+    if (pos < 0 || pos >= a.max_seq) return;
+    const int nact = (pos + 1 + CH - 1) / CH;
+    if (nact == 1) return;  // the attention kernel wrote the output itself (direct_out)
     __syncthreads();
-    if (!last_s) return;
-    if (tid < D) {
+    float M = -INFINITY;
+    for (int sp = 0; sp < nact; ++sp) M = fmaxf(M, m_s[sp]);
+    float lw = 0.f;
+    for (int sp = tid; sp < nact; sp += kThreads) lw = fmaf(l_s[sp], expf(m_s[sp] - M), lw);
+    const float L = block_sum(lw, red_s);
+    float O = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMergeChunk; ++i) {
+        const int sp = half + 2 * i;
+        const float w = sp < nact ? expf(m_s[sp] - M) : 0.f;
+        O = fmaf(sp < nact ? ov[i] : 0.f, w, O);
+    }
+    for (int sp = half + 2 * kMergeChunk; sp < nact; sp += 2) O = fmaf(oh[(size_t)sp * D], expf(m_s[sp] - M), O);
+    o_red[half][d] = O;
+    __syncthreads();
+    if (tid < D) a.out[(size_t)h * D + tid] = (o_red[0][tid] + o_red[1][tid]) / L;
+}
+
+// 8 weights of one W_o row slice as loaded: 16 B (f16), 32 B (f32) or 8 B (i8)
+template <typename WT> struct W8 { uint4 v[sizeof(WT) == 4 ? 2 : 1]; };
+template <typename WT>
+__device__ __forceinline__ W8<WT> ld_w8(const WT* p) {
+    W8<WT> r;
+    if constexpr (sizeof(WT) == 1) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 u = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+        r.v[0] = make_uint4(u.x, u.y, 0, 0);
+    } else {
+        r.v[0] = ld_nt16(p);
+        if constexpr (sizeof(WT) == 4) r.v[1] = ld_nt16(p + 4);
+    }
+    return r;
+}
+template <typename WT>
+__device__ __forceinline__ void unpack_w8(const W8<WT>& r, float* v) {
+    if constexpr (sizeof(WT) == 1) {
+        const uint32_t w[2] = {r.v[0].x, r.v[0].y};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (float)(int8_t)((w[i / 4] >> (8 * (i % 4))) & 0xff);
+    } else if constexpr (sizeof(WT) == 2) {
+        Raw<__half> h;
+        h.v[0] = r.v[0];
+        unpack8(h, v);
+    } else {
+        Raw<float> f;
+        f.v[0] = r.v[0];
+        f.v[1] = r.v[1];
+        unpack8(f, v);
+    }
+}
+
+// Workgroup (h, row chunk of 16 * NPL rows). Prologue issues, before anything waits:
+// its W_o slice loads (NPL rows per 16-lane group, independent of the position),
+// the position, and head h's split partials (one round). Then: log-sum-exp merge
+// (every row chunk of a head repeats it from L2: ~nact * 0.5 KB), 16-lane dot
+// products, and one int64 fixed-point atomic add per output row.
+template <typename WT, int NPL>
+__global__ __launch_bounds__(kThreads) void attn_oproj_kernel(OprojArgs a, int ns) {
+    __shared__ float m_s[kMaxSplits];
+    __shared__ float l_s[kMaxSplits];
+    __shared__ float linv_s;
+    __shared__ __attribute__((aligned(16))) float o_s[D];
+    __shared__ float o_red[2][D];
+    __shared__ float y_s[16 * NPL];
+    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;  // scalar load, issued first
+    const int h = blockIdx.x, tid = threadIdx.x;
+    const int grp = tid / LPR, l16 = tid % LPR;
+    const int row0 = blockIdx.y * 16 * NPL;
+    const WT* w = reinterpret_cast<const WT*>(a.w);
+
+    // issue order: partials first (needed first), then the W_o slice (needed last)
+    Ws ws = ws_carve(const_cast<void*>(a.workspace), a.heads, ns);
+    const int d = tid % D, half = tid / D;
+    const float* mlh = ws.ml + (size_t)h * ns * 2;
+    const float* oh = ws.o + (size_t)h * ns * D + d;
+    float ov[kMergeChunk];
+#pragma unroll
+    for (int i = 0; i < kMergeChunk; ++i) {
+        const int sp = half + 2 * i;
+        ov[i] = oh[(size_t)(sp < ns ? sp : 0) * D];
+    }
+    for (int sp = tid; sp < ns; sp += kThreads) {
+        m_s[sp] = mlh[2 * sp];
+        l_s[sp] = mlh[2 * sp + 1];
+    }
+    W8<WT> wr[NPL];
+#pragma unroll
+    for (int t = 0; t < NPL; ++t) {
+        int row = row0 + grp + 16 * t;
+        row = row < a.n_rows ? row : a.n_rows - 1;
+        wr[t] = ld_w8<WT>(w + (size_t)row * a.ldw + (size_t)h * D + l16 * 8);
+    }
+    if (pos < 0 || pos >= a.max_seq) return;
+    const int nact = (pos + 1 + CH - 1) / CH;
+    __syncthreads();
+    // log-sum-exp weights by wave 0 (one expf per split), into LDS
+    if (tid < kWave) {
         float M = -INFINITY;
-        for (int s = 0; s < nact; ++s) M = fmaxf(M, ws.ml[((size_t)h * ns + s) * 2]);
-        float L = 0.f, O = 0.f;
-        for (int s = 0; s < nact; ++s) {
-            const float w = expf(ws.ml[((size_t)h * ns + s) * 2] - M);
-            L = fmaf(ws.ml[((size_t)h * ns + s) * 2 + 1], w, L);
-            O = fmaf(ws.o[((size_t)h * ns + s) * D + tid], w, O);
+        for (int sp = tid; sp < nact; sp += kWave) M = fmaxf(M, m_s[sp]);
+        M = wave_max(M);
+        float lsum = 0.f;
+        for (int sp = tid; sp < nact; sp += kWave) {
+            const float wgt = expf(m_s[sp] - M);
+            m_s[sp] = wgt;
+            lsum = fmaf(l_s[sp], wgt, lsum);
         }
-        a.out[(size_t)h * D + tid] = O / L;
+        lsum = wave_sum(lsum);
+        if (tid == 0) linv_s = 1.0f / lsum;
     }
-    if (tid == 0) __hip_atomic_store(ws.counters + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    float O = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMergeChunk; ++i) {
+        const int sp = half + 2 * i;
+        O = fmaf(sp < nact ? ov[i] : 0.f, sp < nact ? m_s[sp] : 0.f, O);
+    }
+    for (int sp = half + 2 * kMergeChunk; sp < nact; sp += 2) O = fmaf(oh[(size_t)sp * D], m_s[sp], O);
+    o_red[half][d] = O;
+    __syncthreads();
+    if (tid < D) o_s[tid] = (o_red[0][tid] + o_red[1][tid]) * linv_s;
+    __syncthreads();
+
+    float xv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xv[i] = o_s[l16 * 8 + i];
+#pragma unroll
+    for (int t = 0; t < NPL; ++t) {
+        float wv[8];
+        unpack_w8<WT>(wr[t], wv);
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc = fmaf(wv[i], xv[i], acc);
+#pragma unroll
+        for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+        if (l16 == 0) y_s[grp + 16 * t] = acc;
+    }
+    __syncthreads();
+    if (tid < 16 * NPL) {
+        const int row = row0 + tid;
+        if (row < a.n_rows) {
+            float v = y_s[tid];
+            if (a.scales) v *= __half2float(a.scales[row]);
+            atomicAdd(reinterpret_cast<unsigned long long*>(a.xacc + row), (unsigned long long)to_fixed(v));
+        }
+    }
+}
+
+template <typename WT>
+int oproj_launch_w(const OprojArgs& a, hipStream_t s) {
+    // ~1024 workgroups: rows per workgroup = 16 * NPL
+    const long target = (long)a.heads * a.n_rows / (1024 * 16);
+    const int ns = (a.max_seq + CH - 1) / CH;
+    const int npl = target >= 8 ? 8 : target >= 4 ? 4 : target >= 2 ? 2 : 1;
+    const dim3 grid(a.heads, (a.n_rows + 16 * npl - 1) / (16 * npl));
+    switch (npl) {
+        case 8: hipLaunchKernelGGL((attn_oproj_kernel<WT, 8>), grid, dim3(kThreads), 0, s, a, ns); break;
+        case 4: hipLaunchKernelGGL((attn_oproj_kernel<WT, 4>), grid, dim3(kThreads), 0, s, a, ns); break;
+        case 2: hipLaunchKernelGGL((attn_oproj_kernel<WT, 2>), grid, dim3(kThreads), 0, s, a, ns); break;
+        default: hipLaunchKernelGGL((attn_oproj_kernel<WT, 1>), grid, dim3(kThreads), 0, s, a, ns); break;
+    }
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
 }
 
 }  // namespace
@@ -256,10 +492,12 @@ size_t attn_workspace_bytes(int heads, int head_dim, int max_seq) {
 int attn_decode_launch(const AttnArgs& a, hipStream_t s) {
     LLMI_REQUIRE(a.head_dim == D, "attn: head_dim must be 128");
     LLMI_REQUIRE(a.heads > 0 && a.kv_heads > 0 && a.heads % a.kv_heads == 0, "attn: bad head counts");
-    LLMI_REQUIRE(a.max_seq > 0, "attn: max_seq must be > 0");
+    LLMI_REQUIRE(a.max_seq > 0 && (a.max_seq + CH - 1) / CH <= kMaxSplits, "attn: max_seq out of range");
     LLMI_REQUIRE(a.pos_dev || (a.pos_host >= 0 && a.pos_host < a.max_seq), "attn: pos out of range");
-    LLMI_REQUIRE(a.qkv && a.k_cache && a.v_cache && a.out && a.workspace, "attn: null pointer");
-    const dim3 grid(a.heads, (a.max_seq + CH - 1) / CH);
+    LLMI_REQUIRE(a.qkv && a.k_cache && a.v_cache && a.workspace, "attn: null pointer");
+    LLMI_REQUIRE(!a.direct_out || a.out, "attn: null output");
+    LLMI_REQUIRE(!a.xacc || a.resid, "attn: xacc seeding needs resid");
+    const dim3 grid(a.heads, (a.max_seq + CH - 1) / CH);  // ns = gridDim.y
     if (a.cache_dtype == LLMI_F16)
         hipLaunchKernelGGL(attn_decode_kernel<__half>, grid, dim3(kThreads), 0, s, a);
     else if (a.cache_dtype == LLMI_F32)
@@ -267,7 +505,26 @@ int attn_decode_launch(const AttnArgs& a, hipStream_t s) {
     else
         LLMI_REQUIRE(false, "attn: cache dtype must be f16 or f32");
     LLMI_HIP(hipGetLastError());
+    if (a.direct_out) {
+        hipLaunchKernelGGL(attn_merge_kernel, dim3(a.heads), dim3(kThreads), 0, s, a, (int)grid.y);
+        LLMI_HIP(hipGetLastError());
+    }
     return LLMI_OK;
+}
+
+int attn_oproj_launch(const OprojArgs& a, hipStream_t s) {
+    LLMI_REQUIRE(a.head_dim == D, "attn_oproj: head_dim must be 128");
+    LLMI_REQUIRE(a.w && a.workspace && a.xacc && a.heads > 0 && a.n_rows > 0, "attn_oproj: bad arguments");
+    LLMI_REQUIRE(a.ldw >= a.heads * D, "attn_oproj: ldw < heads * head_dim");
+    LLMI_REQUIRE(a.max_seq > 0 && (a.max_seq + CH - 1) / CH <= kMaxSplits, "attn_oproj: max_seq out of range");
+    switch (a.w_dtype) {
+        case LLMI_F16: return oproj_launch_w<__half>(a, s);
+        case LLMI_F32: return oproj_launch_w<float>(a, s);
+        case LLMI_I8:
+            LLMI_REQUIRE(a.scales != nullptr, "attn_oproj: int8 weights need scales");
+            return oproj_launch_w<int8_t>(a, s);
+    }
+    LLMI_REQUIRE(false, "attn_oproj: weight dtype must be f16, f32 or i8");
 }
 
 }  // namespace llmi

@@ -33,6 +33,8 @@
 // indices, so every TP degree computes the same model.
 #include <rccl/rccl.h>
 
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -72,9 +74,11 @@ struct Engine {
 
     char* scratch = nullptr;
     float *x = nullptr, *qkv_buf = nullptr, *attn_out = nullptr, *act = nullptr, *logits = nullptr;
+    long long* xacc = nullptr;  // fixed-point residual accumulator of the fused merge+o_proj
     unsigned long long* partials = nullptr;
     int lm_grid = 0;
     void* attn_ws = nullptr;
+    float* rope_tab = nullptr;  // [max_seq][head_dim/2] (cos, sin): modeling_llama.py:130-146 cache
     DecodeState* st = nullptr;
     int32_t *prompt = nullptr, *tokens = nullptr;
 
@@ -205,14 +209,17 @@ struct Engine {
         const size_t o_ws = take(attn_workspace_bytes(hl, c.head_dim, c.max_seq));  // counters first
         const size_t o_st = take(sizeof(DecodeState));
         const size_t o_x = take(H * 4), o_qkv = take((ql + 2 * kvrows) * 4), o_att = take(ql * 4);
+        const size_t o_xacc = take(H * 8);
         const size_t o_act = take((size_t)il * 4), o_log = take((size_t)vl * 4);
         const size_t o_par = take((size_t)lm_grid * 8);
         const size_t o_pr = take((size_t)c.max_seq * 4), o_tok = take((size_t)(c.max_seq + 1) * 4);
+        const size_t o_rope = take((size_t)c.max_seq * c.head_dim * 4);
         LLMI_HIP(hipMalloc(&scratch, off));
         LLMI_HIP(hipMemsetAsync(scratch, 0, off, stream));
         attn_ws = scratch + o_ws;
         st = (DecodeState*)(scratch + o_st);
         x = (float*)(scratch + o_x);
+        xacc = (long long*)(scratch + o_xacc);
         qkv_buf = (float*)(scratch + o_qkv);
         attn_out = (float*)(scratch + o_att);
         act = (float*)(scratch + o_act);
@@ -220,6 +227,22 @@ struct Engine {
         partials = (unsigned long long*)(scratch + o_par);
         prompt = (int32_t*)(scratch + o_pr);
         tokens = (int32_t*)(scratch + o_tok);
+        rope_tab = (float*)(scratch + o_rope);
+        // cos/sin cache with HF's fp32 arithmetic (LlamaRotaryEmbedding._set_cos_sin_cache):
+        // inv_freq = 1 / fp32(base ** (2i/d)) (torch's fp32 pow is correctly rounded),
+        // angle = fp32(pos * inv_freq), cos/sin correctly rounded to fp32
+        std::vector<float> tab((size_t)c.max_seq * c.head_dim);
+        const int half = c.head_dim / 2;
+        for (int i = 0; i < half; ++i) {
+            const float p = (float)std::pow((double)c.rope_base, (double)(2 * i) / (double)c.head_dim);
+            volatile float inv = 1.0f / p;
+            for (int pos = 0; pos < c.max_seq; ++pos) {
+                volatile float ang = (float)pos * inv;
+                tab[((size_t)pos * half + i) * 2 + 0] = (float)std::cos((double)ang);
+                tab[((size_t)pos * half + i) * 2 + 1] = (float)std::sin((double)ang);
+            }
+        }
+        LLMI_HIP(hipMemcpyAsync(rope_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, stream));
         LLMI_HIP(hipStreamSynchronize(stream));
         return LLMI_OK;
     }
@@ -303,17 +326,23 @@ struct Engine {
         a.max_seq = c.max_seq;
         a.pos_dev = &st->cur_pos;
         a.heads = hl; a.kv_heads = kvl; a.head_dim = c.head_dim;
-        a.rope = 1; a.rope_base = c.rope_base;
+        a.rope = 1; a.rope_base = c.rope_base; a.rope_tab = rope_tab;
+        a.direct_out = 0;  // partials -> attn_oproj
+        a.xacc = xacc;
+        a.resid = x;
+        a.resid_scale = (c.tp_rank == 0) ? 1.f : 0.f;  // rank 0 carries the residual into the all-reduce
+        a.hidden = c.hidden;
         a.out = attn_out; a.workspace = attn_ws;
         return a;
     }
-    GemvArgs o_args(int l) const {
+    OprojArgs o_args(int l) const {
         const Layer& L = layers[l];
-        GemvArgs a;
+        OprojArgs a;
         a.w = L.o; a.scales = L.o_s; a.w_dtype = wdt;
-        a.n_rows = c.hidden; a.k = ql; a.x = attn_out;
-        a.epi = (c.tp_rank == 0) ? EPI_ADD : EPI_STORE;  // rank 0 carries the residual into the all-reduce
-        a.y = x; a.resid = x;
+        a.n_rows = c.hidden; a.ldw = ql;
+        a.heads = hl; a.head_dim = c.head_dim; a.max_seq = c.max_seq;
+        a.pos_dev = &st->cur_pos;
+        a.workspace = attn_ws; a.xacc = xacc;
         return a;
     }
     GemvArgs gu_args(int l) const {
@@ -321,7 +350,8 @@ struct Engine {
         GemvArgs a;
         a.w = L.gu; a.scales = L.gu_s; a.w_dtype = wdt;
         a.n_rows = 2 * il; a.k = c.hidden;
-        a.x = x; a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
+        a.x_fixed = xacc; a.x_out = x;  // residual after attention, written back to x by workgroup 0
+        a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
         return a;
     }
@@ -348,8 +378,11 @@ struct Engine {
         for (int l = 0; l < c.layers; ++l) {
             LLMI_TRY(gemv_launch(qkv_args(l), stream));
             LLMI_TRY(attn_decode_launch(attn_args(l), stream));
-            LLMI_TRY(gemv_launch(o_args(l), stream));
-            LLMI_TRY(allreduce_sum(x, c.hidden));
+            LLMI_TRY(attn_oproj_launch(o_args(l), stream));
+            if (comm) {  // exact int64 sum of the fixed-point residual partials
+                ncclResult_t r = ncclAllReduce(xacc, xacc, c.hidden, ncclInt64, ncclSum, comm, stream);
+                LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
+            }
             LLMI_TRY(gemv_launch(gu_args(l), stream));
             LLMI_TRY(gemv_launch(down_args(l), stream));
             LLMI_TRY(allreduce_sum(x, c.hidden));
@@ -581,7 +614,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
         switch (which) {
             case 0: return llmi::gemv_launch(g.qkv_args(0), g.stream);
             case 1: return llmi::attn_decode_launch(g.attn_args(0), g.stream);
-            case 2: return llmi::gemv_launch(g.o_args(0), g.stream);
+            case 2: return llmi::attn_oproj_launch(g.o_args(0), g.stream);
             case 3: return llmi::gemv_launch(g.gu_args(0), g.stream);
             case 4: return llmi::gemv_launch(g.down_args(0), g.stream);
             case 5: return llmi::gemv_launch(g.lm_args(), g.stream);

@@ -28,7 +28,17 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWavesPerBlock = kThreads / kWave;
-constexpr int kUnroll = 8;  // 16-B loads per row in flight per lane
+#ifndef LLMI_GEMV_UNROLL
+#define LLMI_GEMV_UNROLL 8
+#endif
+#ifndef LLMI_GEMV_ROWS
+#define LLMI_GEMV_ROWS 2
+#endif
+#ifndef LLMI_GEMV_MAX_GRID
+#define LLMI_GEMV_MAX_GRID 1024
+#endif
+constexpr int kUnrollMax = LLMI_GEMV_UNROLL;  // 16-B loads per row in flight per lane
+constexpr int kRows = LLMI_GEMV_ROWS;      // rows per wave (EPI_SILU_MUL always pairs 2)
 
 template <typename WT> struct WT_ { };
 template <> struct WT_<__half> { static constexpr int EPL = 8; };
@@ -73,89 +83,155 @@ __device__ __forceinline__ float dot_packet(const uint4& w, const float4* xp, in
     return s;
 }
 
-template <typename GT>
-__device__ __forceinline__ float gamma_at(const void* g, int i) {
-    return to_f32(reinterpret_cast<const GT*>(g)[i]);
-}
-
 __device__ __forceinline__ float silu(float v) { return v / (1.0f + expf(-v)); }
 
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT>
-__global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs a) {
+template <typename GT>
+__device__ __forceinline__ float4 gamma4(const void* g, int j) {
+    if constexpr (sizeof(GT) == 2) {
+        const uint2 u = reinterpret_cast<const uint2*>(g)[j];
+        const float2 a = __half22float2(*reinterpret_cast<const __half2*>(&u.x));
+        const float2 b = __half22float2(*reinterpret_cast<const __half2*>(&u.y));
+        return make_float4(a.x, a.y, b.x, b.y);
+    } else {
+        return reinterpret_cast<const float4*>(g)[j];
+    }
+}
+
+// XPT: float4s of x each thread holds in registers during staging (k <= XPT*4*256);
+// 0 = generic strided staging (no weight prefetch).
+#ifndef LLMI_GEMV_MIN_WAVES
+#define LLMI_GEMV_MIN_WAVES 1  // min waves per SIMD (launch-bounds 2nd arg): caps VGPRs
+#endif
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX>
+__global__ __launch_bounds__(kThreads, LLMI_GEMV_MIN_WAVES) void gemv_kernel(GemvArgs a) {
     constexpr int EPL = WT_<WT>::EPL;
     constexpr int PK = EPL / 4;                 // float4 packets per 16-B weight load
     // all LDS in one 16-B aligned dynamic region (cdna_hip_programming.md G17):
     // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
     const int k = a.k;
+    const int k4 = k / 4;
     const int nc = k / EPL;                     // 16-B chunks per row
-    float* red = reinterpret_cast<float*>(xs + k / 4);
+    float* red = reinterpret_cast<float*>(xs + k4);
     unsigned long long* best_s = reinterpret_cast<unsigned long long*>(red + 16);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-    // ---- stage x (packet-major), optional RMSNorm prologue
-    const float4* x4 = reinterpret_cast<const float4*>(a.x);
-    float ss = 0.f;
-    for (int j = tid; j < k / 4; j += kThreads) {
-        float4 v = x4[j];
-        if (NORM) ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-        xs[(j % PK) * nc + j / PK] = v;
-    }
-    if (NORM) {
-        ss = block_sum(ss, red);  // includes __syncthreads
-        const float rstd = 1.0f / sqrtf(ss / (float)k + a.eps);
-        for (int j = tid; j < k / 4; j += kThreads) {
-            const int slot = (j % PK) * nc + j / PK;
-            float4 v = xs[slot];
-            v.x = gamma_at<GT>(a.gamma, 4 * j + 0) * (v.x * rstd);
-            v.y = gamma_at<GT>(a.gamma, 4 * j + 1) * (v.y * rstd);
-            v.z = gamma_at<GT>(a.gamma, 4 * j + 2) * (v.z * rstd);
-            v.w = gamma_at<GT>(a.gamma, 4 * j + 3) * (v.w * rstd);
-            xs[slot] = v;
-        }
-    }
-    __syncthreads();
-
     const int n_groups = (EPI == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + ROWS - 1) / ROWS;
     const char* wbase = reinterpret_cast<const char*>(a.w);
     const size_t row_bytes = (size_t)k * sizeof(WT);
-    unsigned long long best = 0ull;
+    const float4* x4 = reinterpret_cast<const float4*>(a.x);
 
-    for (int g = blockIdx.x * kWavesPerBlock + wave; g < n_groups; g += gridDim.x * kWavesPerBlock) {
-        int rows[ROWS];
+    auto rows_of = [&](int g, int* rows) {
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r)
-            rows[r] = (EPI == EPI_SILU_MUL) ? g + r * a.pair_off : g * ROWS + r;
-        float acc[ROWS];
+        for (int r = 0; r < ROWS; ++r) rows[r] = (EPI == EPI_SILU_MUL) ? g + r * a.pair_off : g * ROWS + r;
+    };
+    // Branch-free streaming: every lane always issues its ROWS x kUnroll loads; out of
+    // range chunks/rows are clamped to a valid address and zeroed by a mask. A
+    // predicated load makes hipcc branch around each load and wait vmcnt(0) per load
+    // (cdna_hip_programming.md §5 "three .s-level traps" (c)), serialising the stream.
+    auto load_batch = [&](uint4 (&wv)[ROWS][kUnroll], const int* rows, int base) {
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
-
-        for (int base = 0; base < nc; base += kWave * kUnroll) {
-            uint4 wv[ROWS][kUnroll];
+        for (int u = 0; u < kUnroll; ++u) {
+            const int c = base + u * kWave + lane;
+            const int cc = c < nc ? c : nc - 1;
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int c = base + u * kWave + lane;
-#pragma unroll
-                for (int r = 0; r < ROWS; ++r) {
-                    if (c < nc && rows[r] < a.n_rows)
-                        wv[r][u] = ld_nt16(wbase + (size_t)rows[r] * row_bytes + (size_t)c * 16);
-                    else
-                        wv[r][u] = make_uint4(0, 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int c = base + u * kWave + lane;
-                if (c < nc) {
-                    const float4* xp = xs + c;
-#pragma unroll
-                    for (int r = 0; r < ROWS; ++r) acc[r] += dot_packet(wv[r][u], xp, nc, (WT*)nullptr);
-                }
+            for (int r = 0; r < ROWS; ++r) {
+                const int rr = rows[r] < a.n_rows ? rows[r] : a.n_rows - 1;
+                const unsigned m = (c < nc && rows[r] < a.n_rows) ? 0xFFFFFFFFu : 0u;
+                uint4 v = ld_nt16(wbase + (size_t)rr * row_bytes + (size_t)cc * 16);
+                v.x &= m; v.y &= m; v.z &= m; v.w &= m;
+                wv[r][u] = v;
             }
         }
+    };
+    auto dot_batch = [&](const uint4 (&wv)[ROWS][kUnroll], int base, float* acc) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int c = base + u * kWave + lane;
+            const float4* xp = xs + (c < nc ? c : nc - 1);  // masked chunks have zero weights
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) acc[r] += dot_packet(wv[r][u], xp, nc, (WT*)nullptr);
+        }
+    };
+
+    // ---- prologue. Issue order matters: vmcnt retires loads in issue order, so x
+    // (and gamma) go first, then this wave's first weight batch; the weight stream is
+    // then in flight while x is staged and the norm is reduced.
+    const int g0 = blockIdx.x * kWavesPerBlock + wave;
+    int rows0[ROWS];
+    rows_of(g0, rows0);
+    uint4 w0[ROWS][kUnroll];
+    float ss = 0.f;
+    const bool wb = XFIX && blockIdx.x == 0 && a.x_out != nullptr;  // one block writes x back
+    if constexpr (XPT > 0) {
+        // branch-free: clamp the index, load, and predicate only the LDS store
+        float4 xv[XPT], gv[XPT];
+        longlong2 xf[XFIX ? XPT : 1][2];
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            int j = tid + i * kThreads;
+            j = j < k4 ? j : k4 - 1;
+            if constexpr (XFIX) {
+                xf[i][0] = reinterpret_cast<const longlong2*>(a.x_fixed)[2 * j];
+                xf[i][1] = reinterpret_cast<const longlong2*>(a.x_fixed)[2 * j + 1];
+            } else {
+                xv[i] = x4[j];
+            }
+            if (NORM) gv[i] = gamma4<GT>(a.gamma, j);
+        }
+        load_batch(w0, rows0, 0);
+        // RMSNorm (modeling_llama.py:112-117) as gamma*x staged + one scalar rsqrt per
+        // dot product in the epilogue: sum_k W[r,k] gamma_k x_k * rstd.
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int j = tid + i * kThreads;
+            if (j < k4) {
+                float4 v;
+                if constexpr (XFIX) {
+                    v = make_float4(from_fixed(xf[i][0].x), from_fixed(xf[i][0].y),
+                                    from_fixed(xf[i][1].x), from_fixed(xf[i][1].y));
+                    if (wb) reinterpret_cast<float4*>(a.x_out)[j] = v;
+                } else {
+                    v = xv[i];
+                }
+                if (NORM) {
+                    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                    v.x *= gv[i].x; v.y *= gv[i].y; v.z *= gv[i].z; v.w *= gv[i].w;
+                }
+                xs[(j % PK) * nc + j / PK] = v;
+            }
+        }
+    } else {
+        for (int j = tid; j < k4; j += kThreads) {
+            float4 v;
+            if constexpr (XFIX) {
+                const long long* f = a.x_fixed + 4 * j;
+                v = make_float4(from_fixed(f[0]), from_fixed(f[1]), from_fixed(f[2]), from_fixed(f[3]));
+                if (wb) reinterpret_cast<float4*>(a.x_out)[j] = v;
+            } else {
+                v = x4[j];
+            }
+            if (NORM) {
+                const float4 gg = gamma4<GT>(a.gamma, j);
+                ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                v.x *= gg.x; v.y *= gg.y; v.z *= gg.z; v.w *= gg.w;
+            }
+            xs[(j % PK) * nc + j / PK] = v;
+        }
+        load_batch(w0, rows0, 0);
+    }
+    float rstd = 1.f;
+    if (NORM) {
+        ss = block_sum(ss, red);  // its barriers also publish xs
+        rstd = 1.0f / sqrtf(ss / (float)k + a.eps);
+    } else {
+        __syncthreads();
+    }
+
+    unsigned long long best = 0ull;
+    auto finish = [&](int g, const int* rows, float* acc) {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
-            acc[r] = wave_sum(acc[r]);
+            acc[r] = wave_sum(acc[r]) * rstd;
             if (a.scales != nullptr && rows[r] < a.n_rows) acc[r] *= __half2float(a.scales[rows[r]]);
         }
         if (EPI == EPI_SILU_MUL) {
@@ -176,6 +252,34 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs a) {
                 }
             }
         }
+    };
+
+    // ---- first group (its first batch is already in flight)
+    if (g0 < n_groups) {
+        float acc[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+        dot_batch(w0, 0, acc);
+        for (int base = kWave * kUnroll; base < nc; base += kWave * kUnroll) {
+            uint4 wv[ROWS][kUnroll];
+            load_batch(wv, rows0, base);
+            dot_batch(wv, base, acc);
+        }
+        finish(g0, rows0, acc);
+    }
+    // ---- remaining groups
+    for (int g = g0 + gridDim.x * kWavesPerBlock; g < n_groups; g += gridDim.x * kWavesPerBlock) {
+        int rows[ROWS];
+        rows_of(g, rows);
+        float acc[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+        for (int base = 0; base < nc; base += kWave * kUnroll) {
+            uint4 wv[ROWS][kUnroll];
+            load_batch(wv, rows, base);
+            dot_batch(wv, base, acc);
+        }
+        finish(g, rows, acc);
     }
     if (EPI == EPI_ARGMAX) {
         if (lane == 0) best_s[wave] = best;
@@ -188,12 +292,43 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(GemvArgs a) {
     }
 }
 
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT>
-int launch_t(const GemvArgs& a, int grid, hipStream_t s) {
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int U, bool XF>
+int launch_u(const GemvArgs& a, int grid, hipStream_t s) {
     const size_t lds = (size_t)a.k * sizeof(float) + 16 * sizeof(float) + kWavesPerBlock * 8;
-    hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT>), dim3(grid), dim3(kThreads), lds, s, a);
+    const int k4 = a.k / 4;
+    if (k4 <= 4 * kThreads)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 4, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k4 <= 5 * kThreads)  // 13B hidden (5120)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 5, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k4 <= 11 * kThreads)  // 7B inter (11008)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 11, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k4 <= 14 * kThreads)  // 13B inter (13824)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 14, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 0, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
+}
+
+// Loads in flight per wave: measured on MI355X (tools/tune_gemv.sh, profiles/):
+// with many row groups per CU (q/k/v, gate_up) 2 rows x 4 loads per wave win
+// (more waves resident); with few groups (o, down: 2048 pairs; lm_head argmax)
+// 2 rows x 8 loads per wave win.
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT>
+int launch_t(const GemvArgs& a, int grid, hipStream_t s) {
+    const int groups = (EPI == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + ROWS - 1) / ROWS;
+    if constexpr (EPI == EPI_SILU_MUL && NORM) {
+        // the engine's gate_up reads the residual from the fixed-point accumulator
+        if (a.x_fixed) {
+            if (groups >= 4096 && groups <= 12288 && kUnrollMax >= 4)
+                return launch_u<WT, ROWS, EPI, NORM, GT, 4, true>(a, grid, s);
+            return launch_u<WT, ROWS, EPI, NORM, GT, kUnrollMax, true>(a, grid, s);
+        }
+    }
+    LLMI_REQUIRE(a.x_fixed == nullptr, "gemv: fixed-point x only with rmsnorm + silu_mul");
+    if (EPI != EPI_ARGMAX && groups >= 4096 && groups <= 12288 && kUnrollMax >= 4)
+        return launch_u<WT, ROWS, EPI, NORM, GT, 4, false>(a, grid, s);
+    return launch_u<WT, ROWS, EPI, NORM, GT, kUnrollMax, false>(a, grid, s);
 }
 
 template <typename WT, int ROWS, int EPI>
@@ -207,10 +342,10 @@ int launch_norm(const GemvArgs& a, int grid, hipStream_t s) {
 template <typename WT>
 int launch_epi(const GemvArgs& a, int grid, hipStream_t s) {
     switch (a.epi) {
-        case EPI_STORE: return launch_norm<WT, 2, EPI_STORE>(a, grid, s);
-        case EPI_ADD: return launch_norm<WT, 2, EPI_ADD>(a, grid, s);
+        case EPI_STORE: return launch_norm<WT, kRows, EPI_STORE>(a, grid, s);
+        case EPI_ADD: return launch_norm<WT, kRows, EPI_ADD>(a, grid, s);
         case EPI_SILU_MUL: return launch_norm<WT, 2, EPI_SILU_MUL>(a, grid, s);
-        case EPI_ARGMAX: return launch_norm<WT, 2, EPI_ARGMAX>(a, grid, s);
+        case EPI_ARGMAX: return launch_norm<WT, kRows, EPI_ARGMAX>(a, grid, s);
     }
     LLMI_REQUIRE(false, "gemv: bad epilogue");
 }
@@ -221,10 +356,10 @@ int epl_of(int dt) { return dt == LLMI_F16 ? 8 : dt == LLMI_F32 ? 4 : dt == LLMI
 
 int gemv_grid(const GemvArgs& a) {
     if (a.grid > 0) return a.grid;
-    const int groups = (a.epi == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + 1) / 2;
+    const int groups = (a.epi == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + kRows - 1) / kRows;
     int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    // cap: ~4 workgroups per CU on 256 CUs; waves then loop over several row groups
-    return blocks < 1024 ? blocks : 1024;
+    // cap (default ~4 workgroups per CU on 256 CUs); waves then loop over several row groups
+    return blocks < LLMI_GEMV_MAX_GRID ? blocks : LLMI_GEMV_MAX_GRID;
 }
 
 int gemv_launch(const GemvArgs& a, hipStream_t s) {
@@ -232,7 +367,7 @@ int gemv_launch(const GemvArgs& a, hipStream_t s) {
     LLMI_REQUIRE(epl > 0, "gemv: weight dtype must be f16, f32 or i8");
     LLMI_REQUIRE(a.k > 0 && a.k % epl == 0, "gemv: k must be a positive multiple of 16 bytes of weights");
     LLMI_REQUIRE((size_t)a.k * 4 <= 150 * 1024, "gemv: k too large for LDS staging");
-    LLMI_REQUIRE(a.w && a.x && a.y, "gemv: null pointer");
+    LLMI_REQUIRE(a.w && (a.x || a.x_fixed) && a.y, "gemv: null pointer");
     LLMI_REQUIRE(a.w_dtype != LLMI_I8 || a.scales, "gemv: int8 weights need per-row scales");
     LLMI_REQUIRE(a.epi != EPI_ADD || a.resid, "gemv: EPI_ADD needs resid");
     LLMI_REQUIRE(a.epi != EPI_ARGMAX || a.partials, "gemv: EPI_ARGMAX needs partials");

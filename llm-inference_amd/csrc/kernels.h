@@ -1,6 +1,8 @@
 // Internal kernel launch interface (C++). The public C ABI (include/llmi.h)
 // and the decode engine (engine.hip) are both built on these.
 #pragma once
+#include <cmath>
+
 #include "common.h"
 
 namespace llmi {
@@ -20,6 +22,8 @@ struct GemvArgs {
     int n_rows = 0;                // rows of W
     int k = 0;
     const float* x = nullptr;      // [k]
+    const long long* x_fixed = nullptr;  // alternative x source: int64 fixed point (value * 2^32)
+    float* x_out = nullptr;        // with x_fixed: workgroup 0 writes the fp32 x here
     // prologue: optional RMSNorm of x (gamma dtype g_dtype), x_add: x += x_add first
     const void* gamma = nullptr;
     int g_dtype = LLMI_F16;
@@ -50,9 +54,48 @@ struct AttnArgs {
     int heads = 0, kv_heads = 0, head_dim = 128;
     int rope = 1;
     float rope_base = 10000.f;
+    const float* rope_tab = nullptr;  // [max_seq][D/2] (cos, sin) pairs; else computed in-kernel
     float* out = nullptr;          // [heads * D]
     void* workspace = nullptr;
+    // 1 (operator API): normalized output in `out` (merge kernel when > 1 split);
+    // 0 (engine): split partials only, consumed by attn_oproj_launch
+    int direct_out = 1;
+    // engine: seed the fixed-point residual accumulator (see attn_oproj_launch)
+    long long* xacc = nullptr;
+    const float* resid = nullptr;
+    float resid_scale = 1.f;
+    int hidden = 0;
 };
+
+// Merge of the split partials fused into the o_proj, split by head: workgroup
+// (h, row chunk) merges head h's partials and adds W_o[rows, h*d:(h+1)*d] . o_h into
+// xacc[rows] with int64 fixed-point atomics (exact, so the sum is independent of
+// arrival order: deterministic). xacc was seeded by the attention kernel.
+struct OprojArgs {
+    const void* w = nullptr;        // W_o (rank shard): [n_rows, ldw] row-major
+    const __half* scales = nullptr; // int8 per-row scales
+    int w_dtype = LLMI_F16;
+    int n_rows = 0, ldw = 0;
+    int heads = 0, head_dim = 128;
+    int max_seq = 0;
+    const int* pos_dev = nullptr;
+    int pos_host = 0;
+    const void* workspace = nullptr;  // attention partials
+    long long* xacc = nullptr;
+};
+int attn_oproj_launch(const OprojArgs& a, hipStream_t s);
+
+// fixed-point residual accumulator: value = int64 * 2^-32
+__host__ __device__ __forceinline__ long long to_fixed(float v) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __float2ll_rn(v * 4294967296.0f);
+#else
+    return (long long)std::llrintf(v * 4294967296.0f);
+#endif
+}
+__host__ __device__ __forceinline__ float from_fixed(long long v) {
+    return (float)v * 2.3283064365386963e-10f;  // (float) rounds once; * 2^-32 is exact
+}
 constexpr int kAttnChunk = 64;     // cached positions per workgroup (split-KV)
 size_t attn_workspace_bytes(int heads, int head_dim, int max_seq);
 int attn_decode_launch(const AttnArgs& a, hipStream_t s);

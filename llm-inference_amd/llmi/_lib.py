@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(_HERE)
 REPO = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "lib", "libllmi.so")
+LIB_PATH = os.environ.get("LLMI_LIB_PATH") or os.path.join(PKG, "lib", "libllmi.so")
 HEADER = os.path.join(REPO, "include", "llmi.h")
 
 F32, F16, I8, I32 = 0, 1, 2, 3
