@@ -94,10 +94,10 @@ int llmi_rope_decode(float* qkv, int pos, int heads, int kv_heads, int head_dim,
  * writes k, v of the fused qkv row into the cache slot `pos` of `layer`
  * (cache [layers, kv_heads, max_seq, head_dim], dtype f16 or f32), then
  * out[h] = softmax(q_h . K^T / sqrt(d)) V over positions 0..pos (fp32
- * softmax, split-KV over workgroups with a log-sum-exp merge).
+ * softmax, split-KV over workgroups, log-sum-exp merge in a second launch).
  * rope != 0 additionally applies RoPE to q/k first (the engine's fused form).
- * workspace: >= llmi_attn_workspace_bytes(...) bytes of device memory whose
- * counter region is zero before the first call (it is left zeroed). */
+ * workspace: >= llmi_attn_workspace_bytes(...) bytes of device memory (split
+ * partials; no initialisation needed). */
 size_t llmi_attn_workspace_bytes(int heads, int head_dim, int max_seq);
 int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_dtype, int layer,
                      int max_seq, int pos, int heads, int kv_heads, int head_dim, int rope,
@@ -121,6 +121,14 @@ int llmi_synth_fill(void* out, int out_dtype, int kind, uint64_t seed, uint32_t 
 /* Host (CPU) twin of llmi_synth_fill, for checking the generator without a GPU. */
 int llmi_synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
                          int cols, int row0, int col0, int ld);
+/* Device memory for host-side callers that include no HIP headers (the C++
+ * mirror in include/llmi/): hipMalloc / hipFree / hipMemcpy / hipDeviceSynchronize.
+ * kind: 0 host->device, 1 device->host, 2 device->device. */
+int llmi_device_alloc(void** ptr, size_t bytes);
+int llmi_device_free(void* ptr);
+int llmi_memcpy(void* dst, const void* src, size_t bytes, int kind);
+int llmi_device_sync(void);
+
 /* Synthetic prompt ids (bench config: 8 PRNG ids). Host only. */
 int llmi_synth_prompt(uint64_t seed, int n, int vocab, int32_t* out);
 

@@ -1,0 +1,141 @@
+// The reference's operator API (src/kernels/*.h launchers), same names and
+// argument meaning, implemented over the llmi C ABI (include/llmi.h) -- so code
+// written against Mr-wang27/llm-inference's launchers compiles against this
+// header and runs the MI355X kernels. Activations are TensorWrapper<float>
+// (the reference's working instantiation, user_entry.cpp:21 / llama.h:207);
+// weights may be float, half_t or int8_t (+ per-row scales).
+//
+// Differences, all deliberate and documented per launcher:
+//  * every launcher takes an optional trailing stream (hipStream_t as void*);
+//    the reference stored a stream and never used it (model_utils.h:36);
+//  * errors throw std::runtime_error("[oneLLM][ERROR] ...") immediately (the
+//    reference surfaced them at DeviceSyncAndCheckCudaError, macro.h:98-109);
+//  * launchRMSNorm's decoder_residual really receives the pre-norm x (its kernel
+//    aliased it).
+#pragma once
+#include "tensor.h"
+#include "weights.h"
+
+namespace llmi_detail {
+inline void* attn_workspace(int heads, int head_dim, int max_seq) {
+    thread_local void* ws = nullptr;
+    thread_local size_t cap = 0;
+    const size_t need = llmi_attn_workspace_bytes(heads, head_dim, max_seq);
+    if (need > cap) {
+        if (ws) LLMI_CALL(llmi_device_free(ws));
+        LLMI_CALL(llmi_device_alloc(&ws, need));
+        cap = need;
+    }
+    return ws;
+}
+inline int tokens_of(const Tensor* t) { return t->shape.size() >= 2 ? t->size() / t->shape.back() : 1; }
+}  // namespace llmi_detail
+
+// input_embedding.h:6-9 -- out[t, :] = table[ids[t], :]
+template <typename T>
+void launchInputEmbedding(TensorWrapper<int>* input_ids, TensorWrapper<float>* output, EmbeddingWeight<T>* embed_table,
+                          void* stream = nullptr) {
+    LLM_CHECK_WITH_INFO(embed_table->shape.size() == 2, "embedding table must be [vocab, hidden]");
+    LLMI_CALL(llmi_embedding(input_ids->data, input_ids->size(), embed_table->data,
+                             llmiWeightDtype(getWeightType<T>()), embed_table->shape[0], embed_table->shape[1],
+                             output->data, stream));
+}
+
+// rmsnorm_kernel.h:11-17 -- in place on decoder_out; decoder_residual <- pre-norm x
+template <typename T>
+void launchRMSNorm(TensorWrapper<float>* decoder_out, TensorWrapper<float>* decoder_residual,
+                   LayerNormWeight<T>& attn_norm_weight, float eps, bool is_last = false, void* stream = nullptr) {
+    (void)is_last;
+    const int hidden = decoder_out->shape.back();
+    LLMI_CALL(llmi_rmsnorm(decoder_out->data, decoder_out->data, decoder_residual ? decoder_residual->data : nullptr,
+                           attn_norm_weight.gamma, llmiWeightDtype(getWeightType<T>()),
+                           llmi_detail::tokens_of(decoder_out), hidden, eps, stream));
+}
+
+// fused_addresidual_norm.h:9-15 -- residual += decoder_out (+bias); decoder_out = rmsnorm(residual) * scale
+template <typename T>
+void launchFusedAddBiasResidualRMSNorm(TensorWrapper<float>* residual, TensorWrapper<float>* decoder_out,
+                                       BaseWeight<T>& norm, T* scale, float eps, void* stream = nullptr) {
+    const int hidden = decoder_out->shape.back();
+    const int dt = llmiWeightDtype(getWeightType<T>());
+    LLMI_CALL(llmi_add_residual_rmsnorm(residual->data, decoder_out->data, norm.bias, dt, scale, dt,
+                                        llmi_detail::tokens_of(decoder_out), hidden, eps, stream));
+}
+
+// add_residual.h:8-13 -- decoder_out += residual
+inline void launchAddResidual(TensorWrapper<float>* residual, TensorWrapper<float>* decoder_out, bool is_print = false,
+                              void* stream = nullptr) {
+    (void)is_print;
+    LLMI_CALL(llmi_add_residual(residual->data, decoder_out->data, llmi_detail::tokens_of(decoder_out),
+                                decoder_out->shape.back(), stream));
+}
+
+// act_kernel.h:8-9 -- input [n, 2, inter] (gate, up) -> out [n, inter] = silu(gate) * up
+inline void launchAct(TensorWrapper<float>* input, TensorWrapper<float>* out, void* stream = nullptr) {
+    LLM_CHECK_WITH_INFO(input->shape.size() == 3 && input->shape[1] == 2, "launchAct input must be [n, 2, inter]");
+    LLMI_CALL(llmi_silu_mul(input->data, out->data, input->shape[0], input->shape[2], stream));
+}
+
+// cublasWrapper stand-in: the reference's launchLinearGemm takes one (linear.h:16-22);
+// here it only carries the stream.
+struct cublasWrapper {
+    void* stream = nullptr;
+};
+
+// linear.h:16-22 -- output[m, n] = input[m, k] * weight[n, k]^T. The reference's
+// layers always pass trans_b = true for weights (masked_self_attention.cpp:62);
+// trans_a is not supported (it was unused on the decode path).
+template <typename T>
+void launchLinearGemm(TensorWrapper<float>* input, BaseWeight<T>& weight, TensorWrapper<float>* output,
+                      cublasWrapper* cublas_wrapper = nullptr, bool trans_a = false, bool trans_b = true) {
+    LLM_CHECK_WITH_INFO(!trans_a, "launchLinearGemm: trans_a is not supported");
+    LLM_CHECK_WITH_INFO(trans_b, "launchLinearGemm: weights are [out, in] (trans_b = true)");
+    LLM_CHECK_WITH_INFO(weight.shape.size() == 2, "launchLinearGemm: weight must be 2-D");
+    const int k = weight.shape[1], n = weight.shape[0];
+    const int m = input->size() / k;
+    LLM_CHECK_WITH_INFO(m * k == input->size(), "launchLinearGemm: input size is not a multiple of in_features");
+    LLMI_CALL(llmi_linear(input->data, weight.data, llmiWeightDtype(getWeightType<T>()), weight.scale, output->data,
+                          m, n, k, cublas_wrapper ? cublas_wrapper->stream : nullptr));
+}
+
+// qkv_bias_and_RoPE.h:40-42 -- one decode token, in place on q and k of the fused
+// qkv row [1, qkv_head_num, head_size] at position step - 1 (step: host tensor).
+// The reference assumed MHA (head_num = qkv_head_num / 3, :416); kv_head_num may be given.
+inline void launchRoPE(TensorWrapper<float>* qkv_buf, TensorWrapper<int>* step, LLaMAAttentionStaticParams& params,
+                       int kv_head_num = -1, void* stream = nullptr) {
+    const int qkv_heads = qkv_buf->shape[qkv_buf->shape.size() - 2];
+    const int head_size = qkv_buf->shape.back();
+    const int kv = kv_head_num > 0 ? kv_head_num : qkv_heads / 3;
+    LLMI_CALL(llmi_rope_decode(qkv_buf->data, step->getVal() - 1, qkv_heads - 2 * kv, kv, head_size,
+                               params.rotary_embedding_base, stream));
+}
+
+// fused_decoder_self_attention.h:10-19 -- write k, v of the (already rotated) fused qkv
+// into cache slot step - 1 of layer layer_id, then masked MHA over positions
+// 0..step-1. caches [layers, batch(=1), kv_heads, max_seq, head] f32 or f16 bits.
+template <typename T, typename CT>
+void launchDecoderMaskedMHA(TensorWrapper<float>* qkv_buf, BaseWeight<T>& qkv, TensorWrapper<int>* layer_id,
+                            TensorWrapper<CT>* k_cache, TensorWrapper<CT>* v_cache, TensorWrapper<bool>* finished,
+                            TensorWrapper<int>* step, TensorWrapper<float>* mha_output,
+                            LLaMAAttentionStaticParams& static_params, void* stream = nullptr) {
+    (void)qkv;
+    (void)finished;
+    LLM_CHECK_WITH_INFO(k_cache->shape.size() == 5, "kv cache must be [layers, batch, kv_heads, max_seq, head]");
+    LLM_CHECK_WITH_INFO(k_cache->shape[1] == 1, "batch size 1 only");
+    const int kv = k_cache->shape[2], max_seq = k_cache->shape[3], head = k_cache->shape[4];
+    const int qkv_heads = qkv_buf->shape[qkv_buf->shape.size() - 2];
+    const int heads = qkv_heads - 2 * kv;
+    const int cdt = llmiDtype(getTensorType<CT>());
+    void* ws = llmi_detail::attn_workspace(heads, head, max_seq);
+    LLMI_CALL(llmi_attn_decode(qkv_buf->data, k_cache->data, v_cache->data, cdt, layer_id->getVal(), max_seq,
+                               step->getVal() - 1, heads, kv, head, /*rope=*/0, static_params.rotary_embedding_base,
+                               mha_output->data, ws, stream));
+}
+
+// topK.h:51-56 + sampling.h:12-18 as Llama<T> wires them: beam width 1 and
+// K = 1 (llama.cpp:59, sampling.cu:99), i.e. greedy argmax of probs [1, vocab];
+// final_topk_id receives the token id (device int).
+inline void launchTopKforBeamSearch(TensorWrapper<float>* probs, TensorWrapper<int>* final_topk_id,
+                                    void* stream = nullptr) {
+    LLMI_CALL(llmi_argmax(probs->data, probs->shape.back(), final_topk_id->data, stream));
+}

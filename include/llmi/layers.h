@@ -1,0 +1,276 @@
+// The reference's layer API over the llmi operator launchers:
+//   BaseAllocator / allocator            src/memory/allocator/base_allocator.h:7-31
+//   LlamaLayerWeight<T>                  src/weights/llama/layer_weights.h:8-44
+//   LLaMASelfAttentionLayer<T>::Forward  src/layers/attention/masked_self_attention.h:53
+//   LLaMAFFNLayer<T>::forward            src/layers/ffn/ffn.h:50
+//   LlamaSelfDecoder<T>::forward         src/layers/decoder/self_decoder.h:65
+// Same TensorMap keys ("attention_input", "attention_output", "all_k_cache",
+// "all_v_cache", "step", "layer_id", "finished", "ffn_input", "ffn_output",
+// "decoder_input", "decoder_output") and the same per-layer dataflow
+// (RMSNorm -> attention -> fused residual+RMSNorm -> FFN -> residual,
+// self_decoder.cpp:53-86), launched op by op. The decode step with every op
+// fused and graph-captured is the engine (llmi_engine_*, include/llmi/model.h).
+// Fixes carried relative to the reference: the FFN keys match
+// (#13), layer_id is a valid host tensor per layer (#14), decode FFN scratch is
+// one token (#15), the down weight is [H, I] (#21).
+#pragma once
+#include <cstdlib>
+#include <memory>
+#include <vector>
+
+#include "kernels.h"
+
+class BaseAllocator {
+public:
+    virtual ~BaseAllocator() = default;
+    template <typename T> T* Malloc(T* ptr, size_t size, bool is_host) {
+        return static_cast<T*>(UnifyMalloc(static_cast<void*>(ptr), size, is_host));
+    }
+    virtual void* UnifyMalloc(void* ptr, size_t size, bool is_host = false) = 0;
+    template <typename T> void Free(T* ptr, bool is_host) { UnifyFree(static_cast<void*>(ptr), is_host); }
+    virtual void UnifyFree(void* ptr, bool is_host) = 0;
+};
+
+// Plain device/host allocations (the reference's pooled CudaAllocator policy is out
+// of scope: the engine allocates every buffer once).
+class HipAllocator : public BaseAllocator {
+public:
+    void* UnifyMalloc(void* ptr, size_t size, bool is_host = false) override {
+        (void)ptr;
+        if (is_host) return std::calloc(1, size);
+        void* p = nullptr;
+        LLMI_CALL(llmi_device_alloc(&p, size));
+        return p;
+    }
+    void UnifyFree(void* ptr, bool is_host) override {
+        if (!ptr) return;
+        if (is_host) std::free(ptr);
+        else LLMI_CALL(llmi_device_free(ptr));
+    }
+};
+
+// --------------------------------------------------------------- weights
+template <typename T>
+class LlamaLayerWeight {
+    static_assert(!std::is_same<T, int8_t>::value,
+                  "the layer-by-layer API mirrors Llama<float/half>; W8A16 runs in the engine (llmi_engine_*)");
+
+public:
+    LlamaLayerWeight(int head_num, int kv_head_num, int head_size, int inter_size, WeightType weight_type, bool attn_bias,
+                     BaseAllocator* alloc, int layer_id = 0)
+        : head_num(head_num), kv_head_num(kv_head_num), head_size(head_size), inter_size(inter_size),
+          hidden(head_num * head_size), layer_id(layer_id), alloc(alloc) {
+        (void)attn_bias;
+        LLM_CHECK_WITH_INFO(weight_type == getWeightType<T>(), "weight type does not match T");
+        const int qkv_rows = (head_num + 2 * kv_head_num) * head_size;
+        self_attn_weight.qkv = make({qkv_rows, hidden});
+        self_attn_weight.output = make({hidden, head_num * head_size});
+        ffn_weight.gateAndup = make({2 * inter_size, hidden});
+        ffn_weight.down = make({hidden, inter_size});
+        attn_norm_weight.gamma = static_cast<T*>(alloc->UnifyMalloc(nullptr, sizeof(T) * hidden));
+        ffn_norm_weight.gamma = static_cast<T*>(alloc->UnifyMalloc(nullptr, sizeof(T) * hidden));
+        owned = {attn_norm_weight.gamma, ffn_norm_weight.gamma};
+    }
+    ~LlamaLayerWeight() {
+        for (void* p : owned) alloc->UnifyFree(p, false);
+        for (void* p : owned_w) alloc->UnifyFree(p, false);
+    }
+    // layer_weights.cc:69-146 dummy path -> llmi-prng-v1 synthetic weights (the same
+    // values the engine and the oracle generate for (seed, layer)).
+    void loadWeights(uint64_t seed = 0) {
+        const int H = hidden, q = head_num * head_size, kv = kv_head_num * head_size, I = inter_size;
+        const int dt = llmiWeightDtype(getWeightType<T>());
+        const int kind = LLMI_SYN_LINEAR;
+        auto tid = [&](uint32_t k) { return ((uint32_t)(layer_id + 1) << 8) | k; };
+        auto fill = [&](BaseWeight<T>& w, size_t row_off, uint32_t k, int rows, int cols, int ld) {
+            LLMI_CALL(llmi_synth_fill(w.data + row_off * cols, dt, kind, seed, tid(k), rows, cols, 0, 0, ld, nullptr));
+        };
+        fill(self_attn_weight.qkv, 0, 0, q, H, H);
+        fill(self_attn_weight.qkv, q, 1, kv, H, H);
+        fill(self_attn_weight.qkv, q + kv, 2, kv, H, H);
+        fill(self_attn_weight.output, 0, 3, H, q, q);
+        fill(ffn_weight.gateAndup, 0, 4, I, H, H);
+        fill(ffn_weight.gateAndup, I, 5, I, H, H);
+        fill(ffn_weight.down, 0, 6, H, I, I);
+        LLMI_CALL(llmi_synth_fill(attn_norm_weight.gamma, dt, LLMI_SYN_GAMMA, seed, tid(7), 1, H, 0, 0, H, nullptr));
+        LLMI_CALL(llmi_synth_fill(ffn_norm_weight.gamma, dt, LLMI_SYN_GAMMA, seed, tid(8), 1, H, 0, 0, H, nullptr));
+    }
+    LayerNormWeight<T> attn_norm_weight, ffn_norm_weight;
+    LLaMAattentionWeights<T> self_attn_weight;
+    LLaMAFFNWeights<T> ffn_weight;
+
+private:
+    BaseWeight<T> make(std::vector<int> shape) {
+        BaseWeight<T> w;
+        w.shape = shape;
+        const size_t n = (size_t)shape[0] * shape[1];
+        w.data = static_cast<T*>(alloc->UnifyMalloc(nullptr, n * sizeof(T)));
+        owned_w.push_back(w.data);
+        return w;
+    }
+    int head_num, kv_head_num, head_size, inter_size, hidden, layer_id;
+    BaseAllocator* alloc;
+    std::vector<void*> owned, owned_w;
+};
+
+// ------------------------------------------------------------ attention
+template <typename T>
+class LLaMASelfAttentionLayer {
+public:
+    LLaMASelfAttentionLayer(int head_num, int kv_head_num, int head_size, LLaMAAttentionStaticParams attn_params,
+                            void* stream, cublasWrapper* cublas_wrapper, BaseAllocator* allocator)
+        : head_num(head_num), kv_head_num(kv_head_num), head_size(head_size), hidden(head_num * head_size),
+          attn_static_params(attn_params), stream(stream), cublas_wrapper(cublas_wrapper), allocator(allocator) {}
+    ~LLaMASelfAttentionLayer() { freeBuf(); }
+    LLaMAAttentionStaticParams& GetAttnStaticParams() { return attn_static_params; }
+
+    void allocForForward(LLaMAAttentionDynParams& params) {
+        if (qkv_buf) return;
+        const int qkv_heads = head_num + 2 * kv_head_num;
+        qkv_ptr = allocator->Malloc(qkv_ptr, sizeof(float) * params.batch_size * qkv_heads * head_size, false);
+        mha_ptr = allocator->Malloc(mha_ptr, sizeof(float) * params.batch_size * hidden, false);
+        qkv_buf = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{params.batch_size, qkv_heads, head_size}, qkv_ptr);
+        mha_output = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{params.batch_size, head_num, head_size}, mha_ptr);
+    }
+    void freeBuf() {
+        if (qkv_ptr) allocator->Free(qkv_ptr, false);
+        if (mha_ptr) allocator->Free(mha_ptr, false);
+        qkv_ptr = mha_ptr = nullptr;
+        qkv_buf.reset();
+        mha_output.reset();
+    }
+
+    // masked_self_attention.cpp:54-92: qkv GEMV -> RoPE -> fused KV write + MHA -> o_proj
+    template <typename CT>
+    void Forward(TensorMap& inputs, TensorMap& outputs, LLaMAattentionWeights<T>& weights,
+                 LLaMAAttentionDynParams& params) {
+        allocForForward(params);
+        TensorWrapper<float>* attention_input = inputs["attention_input"]->as<float>();
+        TensorWrapper<float>* attention_output = outputs["attention_output"]->as<float>();
+        TensorWrapper<CT>* key_cache = outputs["all_k_cache"]->as<CT>();
+        TensorWrapper<CT>* value_cache = outputs["all_v_cache"]->as<CT>();
+        TensorWrapper<bool>* finished = inputs["finished"]->as<bool>();
+        TensorWrapper<int>* step = inputs["step"]->as<int>();
+        TensorWrapper<int>* layer_id = inputs["layer_id"]->as<int>();
+        cublasWrapper cw{stream};
+        launchLinearGemm(attention_input, weights.qkv, qkv_buf.get(), cublas_wrapper ? cublas_wrapper : &cw, false, true);
+        launchRoPE(qkv_buf.get(), step, attn_static_params, kv_head_num, stream);
+        launchDecoderMaskedMHA(qkv_buf.get(), weights.qkv, layer_id, key_cache, value_cache, finished, step,
+                               mha_output.get(), attn_static_params, stream);
+        launchLinearGemm(mha_output.get(), weights.output, attention_output, cublas_wrapper ? cublas_wrapper : &cw,
+                         false, true);
+    }
+
+private:
+    int head_num, kv_head_num, head_size, hidden;
+    LLaMAAttentionStaticParams attn_static_params;
+    void* stream;
+    cublasWrapper* cublas_wrapper;
+    BaseAllocator* allocator;
+    float *qkv_ptr = nullptr, *mha_ptr = nullptr;
+    std::unique_ptr<TensorWrapper<float>> qkv_buf, mha_output;
+};
+
+// ------------------------------------------------------------------ FFN
+template <typename T>
+class LLaMAFFNLayer {
+public:
+    LLaMAFFNLayer(int head_num, int head_size, int inter_size, void* stream, cublasWrapper* cublas_wrapper,
+                  BaseAllocator* allocator)
+        : inter_size(inter_size), hidden(head_num * head_size), stream(stream), cublas_wrapper(cublas_wrapper),
+          allocator(allocator) {}
+    ~LLaMAFFNLayer() { freeBuf(); }
+    void allocForForward(int batch_size) {
+        if (SwiGLU_input) return;
+        gu_ptr = allocator->Malloc(gu_ptr, sizeof(float) * batch_size * 2 * inter_size, false);
+        act_ptr = allocator->Malloc(act_ptr, sizeof(float) * batch_size * inter_size, false);
+        SwiGLU_input = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{batch_size, 2, inter_size}, gu_ptr);
+        down_proj_input = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{batch_size, inter_size}, act_ptr);
+    }
+    void freeBuf() {
+        if (gu_ptr) allocator->Free(gu_ptr, false);
+        if (act_ptr) allocator->Free(act_ptr, false);
+        gu_ptr = act_ptr = nullptr;
+        SwiGLU_input.reset();
+        down_proj_input.reset();
+    }
+    // ffn.cpp:52-93: gate_up GEMV -> SiLU*mul -> down GEMV
+    void forward(TensorMap& inputs, TensorMap& outputs, LLaMAFFNWeights<T>& weights, LLaMAAttentionDynParams& params) {
+        allocForForward(params.batch_size);
+        TensorWrapper<float>* ffn_input = inputs["ffn_input"]->as<float>();
+        TensorWrapper<float>* ffn_output = outputs["ffn_output"]->as<float>();
+        cublasWrapper cw{stream};
+        cublasWrapper* c = cublas_wrapper ? cublas_wrapper : &cw;
+        launchLinearGemm(ffn_input, weights.gateAndup, SwiGLU_input.get(), c, false, true);
+        launchAct(SwiGLU_input.get(), down_proj_input.get(), stream);
+        launchLinearGemm(down_proj_input.get(), weights.down, ffn_output, c, false, true);
+    }
+
+private:
+    int inter_size, hidden;
+    void* stream;
+    cublasWrapper* cublas_wrapper;
+    BaseAllocator* allocator;
+    float *gu_ptr = nullptr, *act_ptr = nullptr;
+    std::unique_ptr<TensorWrapper<float>> SwiGLU_input, down_proj_input;
+};
+
+// -------------------------------------------------------------- decoder
+template <typename T>
+class LlamaSelfDecoder {
+public:
+    LlamaSelfDecoder(int head_num, int kv_head_num, int head_size, int inter_size, int num_layer,
+                     const LLaMAAttentionStaticParams& attn_params, float rmsnorm_eps, void* stream,
+                     cublasWrapper* cublas_wrapper, BaseAllocator* allocator)
+        : hidden(head_num * head_size), num_layer(num_layer), rmsnorm_eps(rmsnorm_eps), stream(stream),
+          allocator(allocator),
+          selfAttn(head_num, kv_head_num, head_size, attn_params, stream, cublas_wrapper, allocator),
+          ffn(head_num, head_size, inter_size, stream, cublas_wrapper, allocator) {}
+    ~LlamaSelfDecoder() {
+        if (resid_ptr) allocator->Free(resid_ptr, false);
+    }
+
+    // self_decoder.cpp:23-89 for one token; inputs "decoder_input" [1, H], "step" and
+    // "layer_id" (host int), "finished"; outputs "decoder_output", "all_k_cache", "all_v_cache".
+    template <typename CT>
+    void forward(TensorMap& input_tensors, const std::vector<LlamaLayerWeight<T>*>& layerWeights,
+                 TensorMap& output_tensors, LLaMAAttentionDynParams& dyn_params) {
+        if (!resid_ptr) {
+            resid_ptr = allocator->Malloc(resid_ptr, sizeof(float) * dyn_params.batch_size * hidden, false);
+            decoder_residual = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{dyn_params.batch_size, hidden}, resid_ptr);
+        }
+        TensorWrapper<float>* decoder_input = input_tensors["decoder_input"]->as<float>();
+        TensorWrapper<float>* decoder_output = output_tensors["decoder_output"]->as<float>();
+        int layer = 0;
+        TensorWrapper<int> layer_id(CPU, INT32, {1}, &layer);
+        TensorMap attn_in{{"attention_input", decoder_input}, {"finished", input_tensors["finished"]},
+                          {"step", input_tensors["step"]}, {"layer_id", &layer_id}};
+        TensorMap attn_out{{"attention_output", decoder_output}, {"all_k_cache", output_tensors["all_k_cache"]},
+                           {"all_v_cache", output_tensors["all_v_cache"]}};
+        TensorMap ffn_in{{"ffn_input", decoder_output}}, ffn_out{{"ffn_output", decoder_output}};
+        for (layer = 0; layer < num_layer; ++layer) {
+            LlamaLayerWeight<T>* w = layerWeights[layer];
+            // decoder_input <- RMSNorm(x), residual <- x
+            launchRMSNorm(decoder_input, decoder_residual.get(), w->attn_norm_weight, rmsnorm_eps, false, stream);
+            selfAttn.template Forward<CT>(attn_in, attn_out, w->self_attn_weight, dyn_params);
+            // residual += attention_out; decoder_output <- RMSNorm(residual)
+            BaseWeight<T> no_bias;
+            launchFusedAddBiasResidualRMSNorm(decoder_residual.get(), decoder_output, no_bias, w->ffn_norm_weight.gamma,
+                                              rmsnorm_eps, stream);
+            ffn.forward(ffn_in, ffn_out, w->ffn_weight, dyn_params);
+            launchAddResidual(decoder_residual.get(), decoder_output, false, stream);  // x = residual + ffn_out
+            decoder_input = decoder_output;
+            attn_in.insert("attention_input", decoder_output);
+        }
+    }
+
+private:
+    int hidden, num_layer;
+    float rmsnorm_eps;
+    void* stream;
+    BaseAllocator* allocator;
+    LLaMASelfAttentionLayer<T> selfAttn;
+    LLaMAFFNLayer<T> ffn;
+    float* resid_ptr = nullptr;
+    std::unique_ptr<TensorWrapper<float>> decoder_residual;
+};

@@ -113,6 +113,30 @@ int llmi_synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint
     return synth_fill_host(out, out_dtype, kind, seed, tid, rows, cols, row0, col0, ld);
 }
 
+int llmi_device_alloc(void** ptr, size_t bytes) {
+    LLMI_REQUIRE(ptr != nullptr, "device_alloc: null out pointer");
+    LLMI_HIP(hipMalloc(ptr, bytes));
+    return LLMI_OK;
+}
+
+int llmi_device_free(void* ptr) {
+    if (ptr) LLMI_HIP(hipFree(ptr));
+    return LLMI_OK;
+}
+
+int llmi_memcpy(void* dst, const void* src, size_t bytes, int kind) {
+    LLMI_REQUIRE(kind >= 0 && kind <= 2, "memcpy: kind must be 0 (H2D), 1 (D2H) or 2 (D2D)");
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                           : hipMemcpyDeviceToDevice;
+    LLMI_HIP(hipMemcpy(dst, src, bytes, k));
+    return LLMI_OK;
+}
+
+int llmi_device_sync(void) {
+    LLMI_HIP(hipDeviceSynchronize());
+    return LLMI_OK;
+}
+
 int llmi_synth_prompt(uint64_t seed, int n, int vocab, int32_t* out) {
     LLMI_REQUIRE(out && n >= 0 && vocab > 0, "synth_prompt: bad arguments");
     const uint64_t key = prng::tensor_key(seed, prng::PROMPT);
