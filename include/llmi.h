@@ -187,6 +187,25 @@ llmi_stream_t llmi_engine_stream(llmi_engine* e);
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
 
+/* ---- In-process tensor-parallel group (no reference counterpart: the
+ * reference has no TP). W rank engines with tp_rank 0..W-1 on ONE device and
+ * one stream, stepped phase by phase with an in-place reduction kernel where
+ * the RCCL path all-reduces. RCCL refuses two ranks on one device, so this is
+ * the single-GPU parity harness for the sharded path (per-rank weight shards,
+ * rank-0 residual, vocab-parallel argmax keys). cfg->tp_rank/tp_world are
+ * ignored; the group sets them. Same status codes as the engine. */
+typedef struct llmi_group llmi_group;
+int llmi_group_create(const llmi_config* cfg, int world, int device, llmi_group** out);
+int llmi_group_destroy(llmi_group* g);
+int llmi_group_load_synthetic(llmi_group* g, uint64_t seed);
+int llmi_group_set_prompt(llmi_group* g, const int32_t* ids, int n);
+int llmi_group_decode(llmi_group* g, int n_steps, int use_graph);
+/* tokens as seen by one rank (every rank must agree) */
+int llmi_group_tokens(llmi_group* g, int rank, int32_t* out, int n, int* n_valid);
+/* last logits over the full vocab: the ranks' slices concatenated */
+int llmi_group_logits(llmi_group* g, float* out, int n);
+int llmi_group_hidden(llmi_group* g, int rank, float* out, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,7 @@
 // indices, so every TP degree computes the same model.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -52,6 +53,8 @@ struct Engine {
     llmi_config c{};
     int device = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = true;  // false inside an in-process group (the group's stream)
+    bool grouped = false;    // rank of an in-process TP group: reductions are the group's
     // local (per-rank) dims
     int hl = 0, kvl = 0, ql = 0, kvrows = 0, il = 0, vl = 0;
     int wdt = LLMI_F16;      // linear weight dtype
@@ -96,11 +99,12 @@ struct Engine {
         if (kcache) (void)hipFree(kcache);
         if (vcache) (void)hipFree(vcache);
         if (scratch) (void)hipFree(scratch);
-        if (stream) (void)hipStreamDestroy(stream);
+        if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
     // ---------------------------------------------------------------- setup
-    int init(const llmi_config& cfg, int dev, const void* tp_id) {
+    // ext_stream != nullptr: rank of an in-process group (no RCCL communicator)
+    int init(const llmi_config& cfg, int dev, const void* tp_id, hipStream_t ext_stream = nullptr) {
         c = cfg;
         device = dev;
         const int W = c.tp_world;
@@ -128,8 +132,14 @@ struct Engine {
                      "engine: hidden, q rows per rank and inter per rank must be multiples of 16 bytes");
 
         LLMI_HIP(hipSetDevice(device));
-        LLMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        if (W > 1) {
+        if (ext_stream) {
+            stream = ext_stream;
+            own_stream = false;
+            grouped = true;
+        } else {
+            LLMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        }
+        if (W > 1 && !grouped) {
             LLMI_REQUIRE(tp_id != nullptr, "engine: tp_world > 1 needs the RCCL unique id");
             ncclUniqueId id;
             std::memcpy(&id, tp_id, sizeof(id));
@@ -372,22 +382,36 @@ struct Engine {
         return LLMI_OK;
     }
 
+    // One token = start, L x (attention phase | reduce xacc, ffn phase | reduce x),
+    // head | reduce partials. The phases are separate so that an in-process
+    // group (struct Group) can interleave its ranks between the reductions.
+    int rec_start() {
+        return step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, c.max_seq, stream);
+    }
+    int rec_attn(int l) {
+        LLMI_TRY(gemv_launch(qkv_args(l), stream));
+        LLMI_TRY(attn_decode_launch(attn_args(l), stream));
+        return attn_oproj_launch(o_args(l), stream);
+    }
+    int rec_ffn(int l) {
+        LLMI_TRY(gemv_launch(gu_args(l), stream));
+        return gemv_launch(down_args(l), stream);
+    }
+    int rec_head() { return gemv_launch(lm_args(), stream); }
+
     int record_step() {
-        LLMI_TRY(step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, c.max_seq,
-                                   stream));
+        LLMI_REQUIRE(!grouped, "engine: a group rank is stepped by its group");
+        LLMI_TRY(rec_start());
         for (int l = 0; l < c.layers; ++l) {
-            LLMI_TRY(gemv_launch(qkv_args(l), stream));
-            LLMI_TRY(attn_decode_launch(attn_args(l), stream));
-            LLMI_TRY(attn_oproj_launch(o_args(l), stream));
+            LLMI_TRY(rec_attn(l));
             if (comm) {  // exact int64 sum of the fixed-point residual partials
                 ncclResult_t r = ncclAllReduce(xacc, xacc, c.hidden, ncclInt64, ncclSum, comm, stream);
                 LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
             }
-            LLMI_TRY(gemv_launch(gu_args(l), stream));
-            LLMI_TRY(gemv_launch(down_args(l), stream));
+            LLMI_TRY(rec_ffn(l));
             LLMI_TRY(allreduce_sum(x, c.hidden));
         }
-        LLMI_TRY(gemv_launch(lm_args(), stream));
+        LLMI_TRY(rec_head());
         if (comm) {
             ncclResult_t r = ncclAllReduce(partials, partials, lm_grid, ncclUint64, ncclMax, comm, stream);
             LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(max): ") + ncclGetErrorString(r));
@@ -461,12 +485,100 @@ struct Engine {
     }
 };
 
+// In-process tensor-parallel group: W rank engines (tp_rank 0..W-1) on ONE
+// device and ONE stream, stepped phase by phase with group_reduce_kernel in
+// place of the RCCL all-reduces. RCCL refuses two ranks on one device, so this
+// is how the sharded path (per-rank weights, rank-0 residual, vocab-parallel
+// argmax keys) is parity-tested on a single GPU; numerically it differs from
+// the RCCL path only in the fp32 summation order of the down-proj partials.
+struct Group {
+    std::vector<std::unique_ptr<Engine>> r;
+    hipStream_t stream = nullptr;
+    void** ptrs = nullptr;  // device [3][W]: xacc, x, partials of every rank
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+
+    ~Group() {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        if (graph) (void)hipGraphDestroy(graph);
+        r.clear();
+        if (ptrs) (void)hipFree(ptrs);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    int init(const llmi_config& cfg, int world, int dev) {
+        LLMI_REQUIRE(world >= 1 && world <= 64, "group: world must be 1..64");
+        LLMI_HIP(hipSetDevice(dev));
+        LLMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        for (int i = 0; i < world; ++i) {
+            llmi_config c = cfg;
+            c.tp_rank = i;
+            c.tp_world = world;
+            r.emplace_back(new Engine());
+            LLMI_TRY(r.back()->init(c, dev, nullptr, stream));
+        }
+        std::vector<void*> h(3 * world);
+        for (int i = 0; i < world; ++i) {
+            h[i] = r[i]->xacc;
+            h[world + i] = r[i]->x;
+            h[2 * world + i] = r[i]->partials;
+        }
+        LLMI_HIP(hipMalloc(&ptrs, h.size() * sizeof(void*)));
+        LLMI_HIP(hipMemcpy(ptrs, h.data(), h.size() * sizeof(void*), hipMemcpyHostToDevice));
+        return LLMI_OK;
+    }
+
+    int record_step() {
+        const int W = (int)r.size(), H = r[0]->c.hidden;
+        for (auto& e : r) LLMI_TRY(e->rec_start());
+        for (int l = 0; l < r[0]->c.layers; ++l) {
+            for (auto& e : r) LLMI_TRY(e->rec_attn(l));
+            if (W > 1) LLMI_TRY(group_reduce_launch(ptrs, W, H, 0, stream));
+            for (auto& e : r) LLMI_TRY(e->rec_ffn(l));
+            if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + W, W, H, 1, stream));
+        }
+        for (auto& e : r) LLMI_TRY(e->rec_head());
+        if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + 2 * W, W, r[0]->lm_grid, 2, stream));
+        return LLMI_OK;
+    }
+
+    int decode(int n, int use_graph) {
+        Engine& e0 = *r[0];
+        LLMI_REQUIRE(e0.prompt_len > 0, "group decode: set_prompt first");
+        LLMI_REQUIRE(n >= 0 && e0.host_next_pos + n <= e0.c.max_seq, "group decode: would run past max_seq");
+        if (use_graph && !exec) {
+            LLMI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+            int rc = record_step();
+            hipGraph_t g = nullptr;
+            hipError_t err = hipStreamEndCapture(stream, &g);
+            if (rc != LLMI_OK) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc;
+            }
+            LLMI_HIP(err);
+            graph = g;
+            LLMI_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        }
+        for (int i = 0; i < n; ++i) {
+            if (use_graph)
+                LLMI_HIP(hipGraphLaunch(exec, stream));
+            else
+                LLMI_TRY(record_step());
+        }
+        for (auto& e : r) e->host_next_pos += n;
+        return LLMI_OK;
+    }
+};
+
 }  // namespace llmi
 
 // ============================================================== C ABI (engine)
 using llmi::Engine;
 struct llmi_engine {
     Engine e;
+};
+struct llmi_group {
+    llmi::Group g;
 };
 
 namespace {
@@ -655,6 +767,69 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     LLMI_HIP(hipMemcpy(g.x, save.data(), H * 4, hipMemcpyHostToDevice));
     *avg_us = ms * 1000.f / iters;
     if (bytes) *bytes = b;
+    return LLMI_OK;
+}
+
+// ---- in-process TP group (single-device parity harness for the sharded path)
+int llmi_group_create(const llmi_config* cfg, int world, int device, llmi_group** out) {
+    LLMI_REQUIRE(cfg && out, "group_create: null argument");
+    *out = nullptr;
+    auto h = std::make_unique<llmi_group>();
+    int rc = h->g.init(*cfg, world, device);
+    if (rc != LLMI_OK) return rc;
+    *out = h.release();
+    return LLMI_OK;
+}
+
+int llmi_group_destroy(llmi_group* g) {
+    if (g) {
+        (void)hipSetDevice(g->g.r.empty() ? 0 : g->g.r[0]->device);
+        (void)hipStreamSynchronize(g->g.stream);
+        delete g;
+    }
+    return LLMI_OK;
+}
+
+int llmi_group_load_synthetic(llmi_group* g, uint64_t seed) {
+    LLMI_REQUIRE(g, "null group");
+    for (auto& e : g->g.r) LLMI_TRY(e->load_synthetic(seed));
+    return LLMI_OK;
+}
+
+int llmi_group_set_prompt(llmi_group* g, const int32_t* ids, int n) {
+    LLMI_REQUIRE(g, "null group");
+    for (auto& e : g->g.r) LLMI_TRY(e->set_prompt(ids, n));
+    return LLMI_OK;
+}
+
+int llmi_group_decode(llmi_group* g, int n_steps, int use_graph) {
+    LLMI_REQUIRE(g, "null group");
+    return g->g.decode(n_steps, use_graph);
+}
+
+int llmi_group_tokens(llmi_group* g, int rank, int32_t* out, int n, int* n_valid) {
+    LLMI_REQUIRE(g && (out || n == 0) && rank >= 0 && rank < (int)g->g.r.size(), "group_tokens: bad arguments");
+    return g->g.r[rank]->tokens_out(out, n, n_valid);
+}
+
+int llmi_group_logits(llmi_group* g, float* out, int n) {
+    LLMI_REQUIRE(g && out, "group_logits: null argument");
+    LLMI_HIP(hipStreamSynchronize(g->g.stream));
+    int off = 0;
+    for (auto& e : g->g.r) {  // vocab-parallel slices in rank order = the full vocab
+        const int m = std::min(e->vl, n - off);
+        if (m <= 0) break;
+        LLMI_HIP(hipMemcpy(out + off, e->logits, (size_t)m * 4, hipMemcpyDeviceToHost));
+        off += m;
+    }
+    return LLMI_OK;
+}
+
+int llmi_group_hidden(llmi_group* g, int rank, float* out, int n) {
+    LLMI_REQUIRE(g && out && rank >= 0 && rank < (int)g->g.r.size() && n <= g->g.r[0]->c.hidden,
+                 "group_hidden: bad arguments");
+    LLMI_HIP(hipStreamSynchronize(g->g.stream));
+    LLMI_HIP(hipMemcpy(out, g->g.r[rank]->x, (size_t)n * 4, hipMemcpyDeviceToHost));
     return LLMI_OK;
 }
 

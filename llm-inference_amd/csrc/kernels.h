@@ -135,6 +135,8 @@ int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long lon
                   hipStream_t s);
 
 // ---------------------------------------------------------- synthetic
+// in-place reduction over W rank buffers (device array of pointers); op 0 i64 sum, 1 f32 sum, 2 u64 max
+int group_reduce_launch(void* const* dev_bufs, int W, int n, int op, hipStream_t s);
 int synth_fill_launch(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
                       int cols, int row0, int col0, int ld, hipStream_t s);
 int synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,

@@ -336,6 +336,35 @@ int finalize_launch(DecodeState* st, const unsigned long long* partials, int np,
     return LLMI_OK;
 }
 
+// In-process tensor-parallel group (one device, W rank engines on one stream):
+// the all-reduce of the RCCL path done by one kernel over the W rank buffers,
+// in place, summing in rank order. op: 0 int64 sum, 1 fp32 sum, 2 uint64 max.
+__global__ void group_reduce_kernel(void* const* bufs, int W, int n, int op) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (op == 0) {
+        long long s = 0;
+        for (int r = 0; r < W; ++r) s += static_cast<const long long*>(bufs[r])[i];
+        for (int r = 0; r < W; ++r) static_cast<long long*>(bufs[r])[i] = s;
+    } else if (op == 1) {
+        float s = static_cast<const float*>(bufs[0])[i];
+        for (int r = 1; r < W; ++r) s += static_cast<const float*>(bufs[r])[i];
+        for (int r = 0; r < W; ++r) static_cast<float*>(bufs[r])[i] = s;
+    } else {
+        unsigned long long m = 0;
+        for (int r = 0; r < W; ++r) m = max(m, static_cast<const unsigned long long*>(bufs[r])[i]);
+        for (int r = 0; r < W; ++r) static_cast<unsigned long long*>(bufs[r])[i] = m;
+    }
+}
+
+int group_reduce_launch(void* const* dev_bufs, int W, int n, int op, hipStream_t s) {
+    LLMI_REQUIRE(dev_bufs && W >= 1 && n >= 0 && op >= 0 && op <= 2, "group_reduce: bad arguments");
+    if (n == 0) return LLMI_OK;
+    hipLaunchKernelGGL(group_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dev_bufs, W, n, op);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
 int synth_fill_launch(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows, int cols,
                       int row0, int col0, int ld, hipStream_t s) {
     SynthDesc d;

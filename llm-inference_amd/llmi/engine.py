@@ -121,3 +121,58 @@ class Engine:
         self.decode(len(prompt) + n_new - 1, use_graph)
         toks = self.tokens(len(prompt) + n_new)
         return toks[len(prompt):]
+
+
+class TPGroup:
+    """In-process tensor-parallel group (llmi_group_* in include/llmi.h): `world`
+    rank engines on one device, stepped together, reductions by a kernel in
+    place of RCCL. The single-GPU parity harness for the sharded decode path."""
+
+    def __init__(self, cfg: Config, world: int, device: int = 0):
+        self.cfg, self.world = cfg, world
+        h = C.c_void_p()
+        call("llmi_group_create", C.byref(cfg), world, device, C.byref(h))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().llmi_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def load_synthetic(self, seed: int):
+        call("llmi_group_load_synthetic", self._h, seed)
+
+    def tokens(self, rank: int = 0, n: Optional[int] = None) -> np.ndarray:
+        n = self.cfg.max_seq + 1 if n is None else n
+        out = np.zeros(n, np.int32)
+        valid = C.c_int()
+        call("llmi_group_tokens", self._h, rank, out.ctypes.data, n, C.byref(valid))
+        return out[:min(n, valid.value)]
+
+    def logits(self) -> np.ndarray:
+        out = np.zeros(self.cfg.vocab, np.float32)
+        call("llmi_group_logits", self._h, out.ctypes.data, self.cfg.vocab)
+        return out
+
+    def hidden(self, rank: int = 0) -> np.ndarray:
+        out = np.zeros(self.cfg.hidden, np.float32)
+        call("llmi_group_hidden", self._h, rank, out.ctypes.data, self.cfg.hidden)
+        return out
+
+    def generate(self, prompt, n_new: int, use_graph: bool = True) -> np.ndarray:
+        prompt = np.ascontiguousarray(prompt, np.int32)
+        call("llmi_group_set_prompt", self._h, prompt.ctypes.data, len(prompt))
+        call("llmi_group_decode", self._h, len(prompt) + n_new - 1, 1 if use_graph else 0)
+        return self.tokens(0, len(prompt) + n_new)[len(prompt):]
