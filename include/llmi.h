@@ -167,6 +167,16 @@ int llmi_engine_load_synthetic(llmi_engine* e, uint64_t seed);
 int llmi_engine_set_prompt(llmi_engine* e, const int32_t* ids, int n);
 /* Run n forward steps (one token each). use_graph: replay the captured hipGraph. */
 int llmi_engine_decode(llmi_engine* e, int n_steps, int use_graph);
+/* Prefill (Llama<T>::firstTokenGen, llama.cpp:273-316; LlamaContextDecoder::forward,
+ * context_decoder.cpp:47-143): the next n_tokens prompt rows in one batched pass
+ * (chunks of 512) -- MFMA GEMMs, causal prefill attention, KV slots written --
+ * then the last row's lm_head + argmax. Afterwards the engine is exactly where
+ * n_tokens decode steps would have left it, so llmi_engine_decode continues.
+ * exact = 1: fp32-faithful GEMMs (activations split into two fp16 halves);
+ * exact = 0: activations rounded to fp16 (faster, ~1e-3 relative at 32 layers).
+ * Rows must lie inside the prompt; tp_world must be 1. fp32 weights run the
+ * decode kernels row by row. */
+int llmi_engine_prefill(llmi_engine* e, int n_tokens, int exact);
 /* Block until the engine stream is idle. */
 int llmi_engine_sync(llmi_engine* e);
 /* Tokens[0 .. n) of the sequence so far: prompt ids followed by generated ids

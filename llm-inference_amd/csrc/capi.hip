@@ -57,8 +57,16 @@ int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales
     a.n_rows = n;
     a.k = k;
     a.epi = EPI_STORE;
-    // TODO(prefill): m > 8 belongs on the MFMA GEMM; rows go through the GEMV meanwhile.
-    for (int i = 0; i < m; ++i) {
+    if (m > 8 && gemm_supported(w_dtype, n, k, EPI_STORE) && (k % 4) == 0 &&
+        (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0) {
+        GemmArgs g;  // prefill: MFMA GEMM, fp32-faithful (split activations)
+        g.a = x; g.lda = k;
+        g.w = w; g.w_dtype = w_dtype; g.scales = a.scales;
+        g.m = m; g.n = n; g.k = k; g.split = 2;
+        g.epi = EPI_STORE; g.y = y; g.ldy = n;
+        return gemm_launch(g, STREAM(stream));
+    }
+    for (int i = 0; i < m; ++i) {  // decode rows (and shapes the GEMM tiles do not cover): GEMV
         a.x = x + (size_t)i * k;
         a.y = y + (size_t)i * n;
         LLMI_TRY(gemv_launch(a, STREAM(stream)));

@@ -88,6 +88,10 @@ struct Engine {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     ncclComm_t comm = nullptr;
+    // prefill scratch (allocated on first use): rows of one prefill chunk
+    char* pf = nullptr;
+    int pf_rows = 0;
+    float *pf_x = nullptr, *pf_qkv = nullptr, *pf_o = nullptr, *pf_act = nullptr;
     int host_next_pos = 0, prompt_len = 0;
     uint64_t seed = 0;
 
@@ -99,6 +103,7 @@ struct Engine {
         if (kcache) (void)hipFree(kcache);
         if (vcache) (void)hipFree(vcache);
         if (scratch) (void)hipFree(scratch);
+        if (pf) (void)hipFree(pf);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
@@ -468,6 +473,89 @@ struct Engine {
         return LLMI_OK;
     }
 
+    // ------------------------------------------------------------ prefill
+    // Llama<T>::firstTokenGen (llama.cpp:273-316) / LlamaContextDecoder::forward
+    // (context_decoder.cpp:47-143): prompt rows [p0, p0 + n) in chunks of up to
+    // kPrefillRows through the MFMA GEMMs and the causal prefill attention, KV
+    // slots written; then the last row's final norm + lm_head + argmax, leaving
+    // the decode state exactly where n decode steps would have left it.
+    static constexpr int kPrefillRows = 512;
+
+    int alloc_prefill() {
+        if (pf) return LLMI_OK;
+        pf_rows = std::min(kPrefillRows, c.max_seq);
+        const size_t R = pf_rows, A = 256;
+        size_t off = 0;
+        auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, A); return o; };
+        const size_t ox = take(R * c.hidden * 4), oq = take(R * (ql + 2 * kvrows) * 4), oo = take(R * ql * 4),
+                     oa = take(R * il * 4);
+        LLMI_HIP(hipMalloc(&pf, off));
+        pf_x = (float*)(pf + ox);
+        pf_qkv = (float*)(pf + oq);
+        pf_o = (float*)(pf + oo);
+        pf_act = (float*)(pf + oa);
+        return LLMI_OK;
+    }
+
+    int prefill(int n, int split) {
+        LLMI_REQUIRE(!grouped && c.tp_world == 1, "prefill: tensor-parallel prefill is not supported");
+        LLMI_REQUIRE(prompt_len > 0, "prefill: set_prompt first");
+        LLMI_REQUIRE(n >= 1 && host_next_pos + n <= prompt_len, "prefill: rows must lie inside the prompt");
+        LLMI_REQUIRE(split == 1 || split == 2, "prefill: split must be 1 (fp16 A) or 2 (fp32-faithful)");
+        if (!gemm_supported(wdt, ql + 2 * kvrows, c.hidden, EPI_STORE) || !gemm_supported(wdt, c.hidden, ql, EPI_ADD) ||
+            !gemm_supported(wdt, 2 * il, c.hidden, EPI_SILU_MUL) || !gemm_supported(wdt, c.hidden, il, EPI_ADD))
+            return decode(n, 1);  // fp32 weights / odd shapes: the decode kernels, one row at a time
+        LLMI_TRY(alloc_prefill());
+        const int H = c.hidden, p_begin = host_next_pos;
+        const size_t eb = dtype_size(c.kv_dtype);
+        for (int p0 = p_begin; p0 < p_begin + n; p0 += pf_rows) {
+            const int m = std::min(pf_rows, p_begin + n - p0);
+            LLMI_TRY(embedding_launch(prompt + p0, m, embed, edt, c.vocab, H, pf_x, stream));
+            for (int l = 0; l < c.layers; ++l) {
+                const Layer& L = layers[l];
+                GemmArgs g;
+                g.split = split;
+                g.w_dtype = wdt;
+                g.m = m;
+                // rmsnorm + qkv
+                g.a = pf_x; g.lda = H; g.gamma = L.attn_norm; g.g_dtype = edt; g.eps = c.rms_eps;
+                g.w = L.qkv; g.scales = L.qkv_s; g.n = ql + 2 * kvrows; g.k = H;
+                g.epi = EPI_STORE; g.y = pf_qkv; g.ldy = g.n;
+                LLMI_TRY(gemm_launch(g, stream));
+                // rope + kv write + causal attention
+                PrefillAttnArgs pa;
+                pa.qkv = pf_qkv;
+                pa.k_cache = (char*)kcache + (size_t)l * kv_layer_elems * eb;
+                pa.v_cache = (char*)vcache + (size_t)l * kv_layer_elems * eb;
+                pa.cache_dtype = c.kv_dtype; pa.max_seq = c.max_seq; pa.m = m; pa.p0 = p0;
+                pa.heads = hl; pa.kv_heads = kvl; pa.head_dim = c.head_dim; pa.rope_tab = rope_tab; pa.out = pf_o;
+                LLMI_TRY(prefill_attn_launch(pa, stream));
+                // o_proj + residual
+                g.a = pf_o; g.lda = ql; g.gamma = nullptr;
+                g.w = L.o; g.scales = L.o_s; g.n = H; g.k = ql;
+                g.epi = EPI_ADD; g.y = pf_x; g.ldy = H;
+                LLMI_TRY(gemm_launch(g, stream));
+                // rmsnorm + gate_up + silu * up
+                g.a = pf_x; g.lda = H; g.gamma = L.ffn_norm;
+                g.w = L.gu; g.scales = L.gu_s; g.n = 2 * il; g.k = H;
+                g.epi = EPI_SILU_MUL; g.pair_off = il; g.y = pf_act; g.ldy = il;
+                LLMI_TRY(gemm_launch(g, stream));
+                // down + residual
+                g.a = pf_act; g.lda = il; g.gamma = nullptr;
+                g.w = L.down; g.scales = L.down_s; g.n = H; g.k = il;
+                g.epi = EPI_ADD; g.pair_off = 0; g.y = pf_x; g.ldy = H;
+                LLMI_TRY(gemm_launch(g, stream));
+            }
+            if (p0 + m == p_begin + n) {  // last row -> final norm + lm_head + argmax keys
+                LLMI_HIP(hipMemcpyAsync(x, pf_x + (size_t)(m - 1) * H, (size_t)H * 4, hipMemcpyDeviceToDevice, stream));
+                LLMI_TRY(gemv_launch(lm_args(), stream));
+            }
+        }
+        LLMI_TRY(prefill_finish_launch(st, prompt, tokens, p_begin, n, stream));
+        host_next_pos += n;
+        return LLMI_OK;
+    }
+
     int tokens_out(int32_t* out, int n, int* n_valid) {
         int valid = host_next_pos;
         if (host_next_pos >= prompt_len && host_next_pos < c.max_seq) {
@@ -655,6 +743,12 @@ int llmi_engine_decode(llmi_engine* e, int n_steps, int use_graph) {
     LLMI_REQUIRE(e, "null engine");
     LLMI_HIP(hipSetDevice(e->e.device));
     return e->e.decode(n_steps, use_graph);
+}
+
+int llmi_engine_prefill(llmi_engine* e, int n_tokens, int exact) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.prefill(n_tokens, exact ? 2 : 1);
 }
 
 int llmi_engine_sync(llmi_engine* e) {

@@ -42,6 +42,49 @@ struct GemvArgs {
 int gemv_launch(const GemvArgs& a, hipStream_t s);
 int gemv_grid(const GemvArgs& a);  // blocks gemv_launch will use
 
+// ------------------------------------------------------ prefill GEMM (MFMA)
+// Y[m, n] (op)= sum_k A[m, k] W[n, k] for M prompt rows; see gemm.hip.
+struct GemmArgs {
+    const float* a = nullptr;      // [m, lda] fp32 activations
+    int lda = 0;
+    const void* gamma = nullptr;   // non-null: RMSNorm of each A row folded in (gamma dtype g_dtype)
+    int g_dtype = LLMI_F16;
+    float eps = 1e-5f;
+    const void* w = nullptr;       // [n, k] fp16 or int8
+    const __half* scales = nullptr;  // int8: per-row fp16 scale
+    int w_dtype = LLMI_F16;
+    int m = 0, n = 0, k = 0;
+    int split = 2;                 // 2: fp32-faithful (hi + lo fp16 halves of A); 1: fp16 A
+    int epi = EPI_STORE;           // EPI_STORE, EPI_ADD (y += ..), EPI_SILU_MUL (y[m, g] = silu(g) * up)
+    int pair_off = 0;              // EPI_SILU_MUL: row offset of `up` in W (= n / 2)
+    float* y = nullptr;            // [m, ldy]
+    int ldy = 0;
+    int n_tiles = 0;               // set by gemm_launch
+};
+bool gemm_supported(int w_dtype, int n, int k, int epi);
+int gemm_bm(const GemmArgs& a);
+int gemm_launch(GemmArgs a, hipStream_t s);
+
+// ------------------------------------------------- prefill attention
+// rope + KV-cache write of M rows, then causal attention over cache slots
+// [0, p0 + m] per row; see prefill.hip.
+struct PrefillAttnArgs {
+    float* qkv = nullptr;          // [m, (heads + 2 kv) * D] fp32; q rotated in place
+    void* k_cache = nullptr;       // layer base [kv_heads, max_seq, D]
+    void* v_cache = nullptr;
+    int cache_dtype = LLMI_F16;
+    int max_seq = 0;
+    int m = 0, p0 = 0;
+    int heads = 0, kv_heads = 0, head_dim = 128;
+    const float* rope_tab = nullptr;  // [max_seq][D/2] (cos, sin)
+    float* out = nullptr;          // [m, heads * D]
+};
+int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s);
+// after a prefill of prompt rows [p0, p0 + n): record them as tokens and
+// advance the decode state (next_pos = p0 + n)
+int prefill_finish_launch(struct DecodeState* st, const int32_t* prompt, int32_t* tokens, int p0, int n,
+                          hipStream_t s);
+
 // ------------------------------------------------------------- attention
 struct AttnArgs {
     const float* qkv = nullptr;    // [(heads + 2 kv_heads) * D]

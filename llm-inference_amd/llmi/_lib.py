@@ -61,6 +61,7 @@ _SIGS = {
     "llmi_engine_load_synthetic": (_I, [_P, _U64]),
     "llmi_engine_set_prompt": (_I, [_P, _P, _I]),
     "llmi_engine_decode": (_I, [_P, _I, _I]),
+    "llmi_engine_prefill": (_I, [_P, _I, _I]),
     "llmi_engine_sync": (_I, [_P]),
     "llmi_engine_tokens": (_I, [_P, _P, _I, C.POINTER(_I)]),
     "llmi_engine_logits": (_I, [_P, _P, _I]),

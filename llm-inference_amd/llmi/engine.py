@@ -72,6 +72,9 @@ class Engine:
     def decode(self, n_steps: int, use_graph: bool = True):
         call("llmi_engine_decode", self._h, n_steps, 1 if use_graph else 0)
 
+    def prefill(self, n_tokens: int, exact: bool = True):
+        call("llmi_engine_prefill", self._h, n_tokens, 1 if exact else 0)
+
     def sync(self):
         call("llmi_engine_sync", self._h)
 
@@ -114,11 +117,17 @@ class Engine:
         call("llmi_engine_time_kernel", self._h, self.KERNELS[which], iters, C.byref(us), C.byref(b))
         return us.value, b.value
 
-    def generate(self, prompt, n_new: int, use_graph: bool = True) -> np.ndarray:
-        """Greedy: feed the prompt, produce n_new tokens (Llama<T>::Response)."""
+    def generate(self, prompt, n_new: int, use_graph: bool = True, prefill: bool = False,
+                 exact: bool = True) -> np.ndarray:
+        """Greedy: feed the prompt, produce n_new tokens (Llama<T>::Response).
+        prefill=True runs the prompt as one batched pass (firstTokenGen)."""
         prompt = np.asarray(prompt, np.int32)
         self.set_prompt(prompt)
-        self.decode(len(prompt) + n_new - 1, use_graph)
+        if prefill:
+            self.prefill(len(prompt), exact)
+            self.decode(n_new - 1, use_graph)
+        else:
+            self.decode(len(prompt) + n_new - 1, use_graph)
         toks = self.tokens(len(prompt) + n_new)
         return toks[len(prompt):]
 

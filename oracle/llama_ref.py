@@ -135,6 +135,25 @@ def attention_decode(q: np.ndarray, k_cache: np.ndarray, v_cache: np.ndarray, ct
     return np.einsum("hj,hjd->hd", p.astype(np.float32), v).astype(np.float32)
 
 
+def attention_prefill(q: np.ndarray, k_cache: np.ndarray, v_cache: np.ndarray, p0: int) -> np.ndarray:
+    """Causal attention for M query rows at positions p0..p0+M-1 (modeling_llama.py:417-437
+    with the 4-D causal mask of :1043-1046; build_causal_mask.cu:29 semantics).
+
+    q [M, heads, d]; caches [kv_heads, >= p0+M, d] holding this chunk's k/v."""
+    m, heads, d = q.shape
+    ctx = p0 + m
+    group = heads // k_cache.shape[0]
+    k = np.repeat(k_cache[:, :ctx].astype(np.float32), group, axis=0)
+    v = np.repeat(v_cache[:, :ctx].astype(np.float32), group, axis=0)
+    s = np.einsum("mhd,hjd->hmj", q.astype(np.float32), k) / np.float32(math.sqrt(d))
+    allowed = np.arange(ctx)[None, :] <= (p0 + np.arange(m))[:, None]
+    s = np.where(allowed[None], s, np.float32(-np.inf))
+    s = s - s.max(axis=-1, keepdims=True)
+    pr = np.exp(s)
+    pr = pr / pr.sum(axis=-1, keepdims=True)
+    return np.einsum("hmj,hjd->mhd", pr.astype(np.float32), v).astype(np.float32)
+
+
 def argmax_first(logits: np.ndarray) -> int:
     return int(np.argmax(logits))
 
@@ -279,6 +298,39 @@ class LlamaOracle:
         self.pos = pos + 1
         self.last_hidden = x
         return linear(rmsnorm(x, self.final_norm, self.cfg.rms_eps), self.lm_head)
+
+    def prefill(self, ids: np.ndarray, round_a=None) -> np.ndarray:
+        """Llama<T>::firstTokenGen (llama.cpp:273-316): all prompt rows at once through
+        LlamaContextDecoder (context_decoder.cpp:47-143) -- causal attention, KV slots
+        0..M-1 written -- then final norm + lm_head on the LAST row only (llama.cpp:218-233).
+        Returns the last row's fp32 logits; self.last_hidden_rows holds the residual stream.
+
+        round_a (optional) is applied to every GEMM A operand (normed x, attention output,
+        SiLU product) -- used to size the error of rounding them to the MFMA input type."""
+        c = self.cfg
+        ra = (lambda t: t) if round_a is None else round_a
+        ids = np.asarray(ids)
+        m, p0 = len(ids), self.pos
+        X = self.embed[ids].astype(np.float32)
+        cos, sin = rope_cos_sin(np.arange(p0, p0 + m), c.head_dim, c.rope_base)
+        cos, sin = cos[:, None, :], sin[:, None, :]
+        for l in range(c.layers):
+            W = self.layers[l]
+            qkv = linear(ra(rmsnorm(X, W["attn_norm"], c.rms_eps)), W["qkv"])
+            q = qkv[:, :c.q_rows].reshape(m, c.heads, c.head_dim)
+            k = qkv[:, c.q_rows:c.q_rows + c.kv_rows].reshape(m, c.kv_heads, c.head_dim)
+            v = qkv[:, c.q_rows + c.kv_rows:].reshape(m, c.kv_heads, c.head_dim)
+            q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
+            self.k_cache[l, :, p0:p0 + m] = k.transpose(1, 0, 2).astype(self.kv_dtype)
+            self.v_cache[l, :, p0:p0 + m] = v.transpose(1, 0, 2).astype(self.kv_dtype)
+            attn = attention_prefill(q, self.k_cache[l], self.v_cache[l], p0).reshape(m, -1)
+            X = X + linear(ra(attn), W["o"])
+            gu = linear(ra(rmsnorm(X, W["ffn_norm"], c.rms_eps)), W["gate_up"])
+            X = (X + linear(ra(silu(gu[:, :c.inter]) * gu[:, c.inter:]), W["down"])).astype(np.float32)
+        self.pos = p0 + m
+        self.last_hidden_rows = X
+        self.last_hidden = X[-1]
+        return linear(rmsnorm(X[-1], self.final_norm, c.rms_eps), self.lm_head)
 
     def greedy(self, prompt: np.ndarray, n_new: int):
         """Feed the prompt token by token, then n_new greedy tokens.

@@ -1,0 +1,182 @@
+"""Prefill path on the MI355X: the MFMA GEMM
+(gemm.hip) through launchLinearGemm with M > 8 rows, and the engine's batched
+prompt pass (llmi_engine_prefill = Llama<T>::firstTokenGen) against the
+reference's f6 fixture (modeling_llama.py, seq 512) and against the engine's own
+token-by-token decode of the same prompt.
+
+Bars: GEMM fp32-faithful mode <= 2e-6 rel-L2 vs float64 (integer data: exact);
+logits <= 1e-3 rel-L2 vs the reference (north star); tokens exact."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from llmi import _lib  # noqa: E402
+from llmi.engine import Engine, preset, synth_prompt  # noqa: E402
+from oracle import llama_ref as R  # noqa: E402
+from oracle import prng  # noqa: E402
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DEV = "cuda"
+LOGIT_TOL = 1e-3
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def N(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from llmi import ops as O
+    return O
+
+
+# ------------------------------------------------------------------ GEMM
+def test_gemm_integer_exact_lane_map(ops):
+    """Small integers: every product and sum is exact in fp32, so any lane-map or
+    tile-index error shows as a mismatch (asymmetric operands, ragged M)."""
+    rng = np.random.default_rng(1)
+    m, n, k = 77, 256, 192
+    x = rng.integers(-4, 5, (m, k)).astype(np.float32)
+    w = rng.integers(-3, 4, (n, k)).astype(np.float16)
+    y = N(ops.launchLinearGemm(T(x), T(w)))
+    np.testing.assert_array_equal(y, x @ w.astype(np.float32).T)
+
+
+@pytest.mark.parametrize("m,n,k", [(512, 4096, 4096), (512, 384, 11008), (9, 128, 64), (130, 1536, 512),
+                                   (1000, 256, 4096)])
+def test_gemm_f16_fp32_faithful(ops, m, n, k):
+    rng = np.random.default_rng(m + n + k)
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    w = prng.linear_fp16(5, prng.layer_tid(0, prng.KIND_Q), n, k)
+    y = N(ops.launchLinearGemm(T(x), T(w)))
+    ref = x.astype(np.float64) @ w.astype(np.float64).T
+    r = rel(y, ref)
+    print(f"gemm f16 m={m} n={n} k={k}: rel {r:.2e}")
+    assert r < 2e-6
+
+
+def test_gemm_int8(ops):
+    m, n, k = 512, 640, 5120
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    tid = prng.layer_tid(0, prng.KIND_GATE)
+    w, s = prng.int8_weight(3, tid, n, k), prng.int8_row_scale(3, tid, n)
+    y = N(ops.launchLinearGemm(T(x), T(w), T(s)))
+    ref = x.astype(np.float64) @ R.dequant(w, s).astype(np.float64).T
+    assert rel(y, ref) < 2e-6
+
+
+# ----------------------------------------------------------------- engine
+def test_prefill_matches_reference_f6():
+    """Config 3 shape at 1 layer: 512-row prefill vs modeling_llama.py's logits."""
+    f = np.load(os.path.join(G, "f6_prefill.npz"))
+    cfg = preset("llama2-7b", layers=1, max_seq=520)  # slot 512 holds the first generated id
+    cfg.kv_dtype = _lib.F32
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        e.set_prompt(f["ids"])
+        e.prefill(len(f["ids"]))
+        logits = e.logits()
+        toks = e.tokens()
+    r = rel(logits, f["last_logits"])
+    print(f"f6 prefill (7B width, 1 layer, seq 512) logits rel-L2 vs reference: {r:.3e}")
+    assert r < LOGIT_TOL
+    np.testing.assert_array_equal(toks[:512], f["ids"])
+    assert toks[512] == int(np.argmax(f["last_logits"]))
+
+
+def test_prefill_fast_mode_f6():
+    f = np.load(os.path.join(G, "f6_prefill.npz"))
+    cfg = preset("llama2-7b", layers=1, max_seq=512)
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        e.set_prompt(f["ids"])
+        e.prefill(len(f["ids"]), exact=False)
+        r = rel(e.logits(), f["last_logits"])
+    print(f"f6 prefill fp16-activation mode logits rel-L2 vs reference: {r:.3e}")
+    assert r < 5e-3
+
+
+@pytest.mark.parametrize("name,cfgname,over,wdt", [
+    ("tiny.npz", "tiny", {}, _lib.F16),
+    ("f3_decode.npz", "llama2-7b", dict(layers=2, max_seq=64), _lib.F16),
+    ("f5_int8.npz", "llama2-13b", dict(layers=1, max_seq=32), _lib.I8),
+])
+def test_prefill_then_decode_matches_reference(name, cfgname, over, wdt):
+    f = np.load(os.path.join(G, name))
+    cfg = preset(cfgname, **over)
+    cfg.kv_dtype, cfg.weight_dtype = _lib.F32, wdt
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        toks = e.generate(f["prompt"], len(f["tokens"]), prefill=True)
+        logits = e.logits()
+        kv = (e.kv_slot(0, 0), e.kv_slot(0, 7, True)) if "k_l0_p0" in f.files else None
+    np.testing.assert_array_equal(toks, f["tokens"])
+    r = rel(logits, f["last_logits"])
+    print(f"{name} prefill+decode logits rel-L2 vs reference: {r:.3e}")
+    assert r < LOGIT_TOL
+    if kv is not None:  # slots written by the prefill kernel
+        assert rel(kv[0], f["k_l0_p0"]) < 1e-5
+        assert rel(kv[1], f["v_l0_p7"]) < 1e-5
+
+
+def test_prefill_partial_and_chunked_equals_decode_path():
+    """Prompt 700 > one 512-row chunk, entered as 37 decode steps + a 663-row
+    prefill (p0 > 0, two chunks), vs the all-decode run: same tokens."""
+    cfg = preset("llama2-7b", layers=2, max_seq=1024)
+    prompt = synth_prompt(11, 700, cfg.vocab)
+    with Engine(cfg) as e:
+        e.load_synthetic(4)
+        ref_toks = e.generate(prompt, 12)
+        ref_logits = e.logits()
+        e.set_prompt(prompt)
+        e.decode(37)
+        e.prefill(663)
+        e.decode(11)
+        toks = e.tokens()[700:]
+        logits = e.logits()
+    np.testing.assert_array_equal(toks, ref_toks)
+    r = rel(logits, ref_logits)
+    print(f"chunked prefill vs decode path logits rel-L2: {r:.3e}")
+    assert r < LOGIT_TOL
+
+
+def test_full_7b_prefill_512_matches_decode_path():
+    """Config 3: Llama-2-7B (32 layers, fp16 weights + KV), 512-row prompt."""
+    cfg = preset("llama2-7b", max_seq=640)
+    prompt = synth_prompt(1, 512, cfg.vocab)
+    with Engine(cfg) as e:
+        e.load_synthetic(0)
+        ref_toks = e.generate(prompt, 16)
+        ref_logits = e.logits()
+        toks = e.generate(prompt, 16, prefill=True)
+        logits = e.logits()
+    np.testing.assert_array_equal(toks, ref_toks)
+    r = rel(logits, ref_logits)
+    print(f"full 7B prefill-512 + 15 decode vs decode path logits rel-L2: {r:.3e}")
+    assert r < LOGIT_TOL
+
+
+def test_prefill_rejects_rows_past_prompt():
+    cfg = preset("tiny")
+    with Engine(cfg) as e:
+        e.load_synthetic(1)
+        e.set_prompt(np.arange(1, 9, dtype=np.int32))
+        with pytest.raises(_lib.LlmiError, match="inside the prompt"):
+            e.prefill(9)
