@@ -193,9 +193,15 @@ int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes
 /* hipStream_t the engine launches on. */
 llmi_stream_t llmi_engine_stream(llmi_engine* e);
 /* Time `iters` eager launches of one kernel of layer 0 (HIP events on the
- * engine stream). which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head.
+ * engine stream). which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head,
+ * 6 the whole layer as the dataflow kernel (when the engine uses it).
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
+/* Debug timeline of one dataflow layer launch (layer 0): per workgroup, in
+ * dispatch order, {start, wait passed, end} of the 100 MHz s_memrealtime clock
+ * (3 x uint64 each, max_wg workgroups); phase_wgs[5] receives the workgroups of
+ * the q/k/v, attention, o_proj, gate_up and down phases. */
+int llmi_engine_layer_stamps(llmi_engine* e, uint64_t* out, int max_wg, int* n_wg, int* phase_wgs);
 
 /* ---- In-process tensor-parallel group (no reference counterpart: the
  * reference has no TP). W rank engines with tp_rank 0..W-1 on ONE device and

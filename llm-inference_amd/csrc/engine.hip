@@ -77,7 +77,12 @@ struct Engine {
 
     char* scratch = nullptr;
     float *x = nullptr, *qkv_buf = nullptr, *attn_out = nullptr, *act = nullptr, *logits = nullptr;
-    long long* xacc = nullptr;  // fixed-point residual accumulator of the fused merge+o_proj
+    // Residual stream in int64 fixed point (value * 2^32): res[l % 2] is layer l's input,
+    // xacc the mid-layer accumulator (residual + o_proj), res[(l + 1) % 2] the output
+    // (mid + down). Every residual add is an exact integer add, so sums are
+    // independent of workgroup order and of the TP reduction order.
+    long long* xacc = nullptr;
+    long long* res[2] = {nullptr, nullptr};
     unsigned long long* partials = nullptr;
     int lm_grid = 0;
     void* attn_ws = nullptr;
@@ -88,6 +93,12 @@ struct Engine {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     ncclComm_t comm = nullptr;
+    // dataflow kernels (layer.hip): 0 none, 1 the whole layer as one launch (TP = 1),
+    // 2 attention + merge/o_proj as one launch (the latency-bound pair; any TP)
+    int fuse_mode = 0;
+    bool fused = false;            // fuse_mode == 1
+    int down_ksplit = 1;           // K-slices of the down projection (int64 atomic epilogue)
+    unsigned* layer_cnt = nullptr; // [layers][layer_cnt_words()] counters, zeroed by step_start
     // prefill scratch (allocated on first use): rows of one prefill chunk
     char* pf = nullptr;
     int pf_rows = 0;
@@ -224,17 +235,20 @@ struct Engine {
         const size_t o_ws = take(attn_workspace_bytes(hl, c.head_dim, c.max_seq));  // counters first
         const size_t o_st = take(sizeof(DecodeState));
         const size_t o_x = take(H * 4), o_qkv = take((ql + 2 * kvrows) * 4), o_att = take(ql * 4);
-        const size_t o_xacc = take(H * 8);
+        const size_t o_xacc = take(H * 8), o_res0 = take(H * 8), o_res1 = take(H * 8);
         const size_t o_act = take((size_t)il * 4), o_log = take((size_t)vl * 4);
         const size_t o_par = take((size_t)lm_grid * 8);
         const size_t o_pr = take((size_t)c.max_seq * 4), o_tok = take((size_t)(c.max_seq + 1) * 4);
         const size_t o_rope = take((size_t)c.max_seq * c.head_dim * 4);
+        const size_t o_cnt = take((size_t)c.layers * layer_cnt_words() * 4);
         LLMI_HIP(hipMalloc(&scratch, off));
         LLMI_HIP(hipMemsetAsync(scratch, 0, off, stream));
         attn_ws = scratch + o_ws;
         st = (DecodeState*)(scratch + o_st);
         x = (float*)(scratch + o_x);
         xacc = (long long*)(scratch + o_xacc);
+        res[0] = (long long*)(scratch + o_res0);
+        res[1] = (long long*)(scratch + o_res1);
         qkv_buf = (float*)(scratch + o_qkv);
         attn_out = (float*)(scratch + o_att);
         act = (float*)(scratch + o_act);
@@ -243,6 +257,17 @@ struct Engine {
         prompt = (int32_t*)(scratch + o_pr);
         tokens = (int32_t*)(scratch + o_tok);
         rope_tab = (float*)(scratch + o_rope);
+        layer_cnt = (unsigned*)(scratch + o_cnt);
+        {
+            const char* env = std::getenv("LLMI_FUSED");
+            // LLMI_FUSED=1: whole layer (measured slower than the five launches);
+            // LLMI_FUSED=2: attention + o_proj pair
+            fuse_mode = (wdt == LLMI_F32 || !env) ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : 0;
+            if (fuse_mode == 1 && (c.tp_world != 1 || grouped)) fuse_mode = 2;
+            fused = fuse_mode == 1;
+            const char* ks = std::getenv("LLMI_DOWN_KSPLIT");
+            down_ksplit = ks ? std::max(1, std::atoi(ks)) : (fused ? 4 : 1);
+        }
         // cos/sin cache with HF's fp32 arithmetic (LlamaRotaryEmbedding._set_cos_sin_cache):
         // inv_freq = 1 / fp32(base ** (2i/d)) (torch's fp32 pow is correctly rounded),
         // angle = fp32(pos * inv_freq), cos/sin correctly rounded to fp32
@@ -305,13 +330,18 @@ struct Engine {
     }
 
     // ---------------------------------------------------------- one token
-    GemvArgs lm_args() const {
+    GemvArgs lm_args(bool from_x = false) const {
         GemvArgs a;
         a.w = lm_head;
         a.w_dtype = edt;
         a.n_rows = vl;
         a.k = c.hidden;
-        a.x = x;
+        if (from_x) {
+            a.x = x;
+        } else {
+            a.x_fixed = res[c.layers % 2];  // final residual; fp32 copy to x by workgroup 0
+            a.x_out = x;
+        }
         a.gamma = final_norm;
         a.g_dtype = edt;
         a.eps = c.rms_eps;
@@ -327,7 +357,7 @@ struct Engine {
         GemvArgs a;
         a.w = L.qkv; a.scales = L.qkv_s; a.w_dtype = wdt;
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
-        a.x = x; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
+        a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
         return a;
     }
@@ -344,7 +374,7 @@ struct Engine {
         a.rope = 1; a.rope_base = c.rope_base; a.rope_tab = rope_tab;
         a.direct_out = 0;  // partials -> attn_oproj
         a.xacc = xacc;
-        a.resid = x;
+        a.resid_fixed = res[l % 2];
         a.resid_scale = (c.tp_rank == 0) ? 1.f : 0.f;  // rank 0 carries the residual into the all-reduce
         a.hidden = c.hidden;
         a.out = attn_out; a.workspace = attn_ws;
@@ -366,6 +396,9 @@ struct Engine {
         a.w = L.gu; a.scales = L.gu_s; a.w_dtype = wdt;
         a.n_rows = 2 * il; a.k = c.hidden;
         a.x_fixed = xacc; a.x_out = x;  // residual after attention, written back to x by workgroup 0
+        // hand the mid-layer residual to the layer output accumulator (rank 0 carries it)
+        a.seed_src = xacc; a.seed_dst = res[(l + 1) % 2]; a.seed_n = c.hidden;
+        a.seed_keep = c.tp_rank == 0 ? 1 : 0;
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
         return a;
@@ -375,26 +408,51 @@ struct Engine {
         GemvArgs a;
         a.w = L.down; a.scales = L.down_s; a.w_dtype = wdt;
         a.n_rows = c.hidden; a.k = il; a.x = act;
-        a.epi = (c.tp_rank == 0) ? EPI_ADD : EPI_STORE;
-        a.y = x; a.resid = x;
+        a.epi = EPI_ATOMIC; a.yacc = res[(l + 1) % 2];
+        a.ksplit = (il % (down_ksplit * (16 / (int)wsz))) == 0 ? down_ksplit : 1;
         return a;
     }
 
-    int allreduce_sum(float* buf, size_t n) {
-        if (!comm) return LLMI_OK;
-        ncclResult_t r = ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, comm, stream);
-        LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-        return LLMI_OK;
-    }
 
     // One token = start, L x (attention phase | reduce xacc, ffn phase | reduce x),
     // head | reduce partials. The phases are separate so that an in-process
     // group (struct Group) can interleave its ranks between the reductions.
     int rec_start() {
-        return step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, c.max_seq, stream);
+        return step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, res[0], c.max_seq,
+                                 fuse_mode ? layer_cnt : nullptr, c.layers * layer_cnt_words(), stream);
+    }
+    LayerArgs layer_args(int l) const {
+        LayerArgs L;
+        L.qkv = qkv_args(l);
+        L.attn = attn_args(l);
+        L.o = o_args(l);
+        L.gu = gu_args(l);
+        L.down = down_args(l);
+        L.cnt = layer_cnt + (size_t)l * layer_cnt_words();
+        L.err = &st->error;
+        return L;
+    }
+    // one layer as the dataflow kernel; falls back to the five launches when the
+    // shape has no instantiation (and stays unfused from then on)
+    int rec_layer_fused(int l, bool* done) {
+        *done = false;
+        if (!fused) return LLMI_OK;
+        const int rc = layer_launch(layer_args(l), stream);
+        if (rc == LLMI_EUNSUPPORTED) {
+            fused = false;
+            return LLMI_OK;
+        }
+        LLMI_TRY(rc);
+        *done = true;
+        return LLMI_OK;
     }
     int rec_attn(int l) {
         LLMI_TRY(gemv_launch(qkv_args(l), stream));
+        if (fuse_mode == 2) {
+            const int rc = layer_launch_phases(layer_args(l), 1, 2, stream);
+            if (rc != LLMI_EUNSUPPORTED) return rc;
+            fuse_mode = 0;  // no instantiation for this shape: separate launches from now on
+        }
         LLMI_TRY(attn_decode_launch(attn_args(l), stream));
         return attn_oproj_launch(o_args(l), stream);
     }
@@ -408,13 +466,20 @@ struct Engine {
         LLMI_REQUIRE(!grouped, "engine: a group rank is stepped by its group");
         LLMI_TRY(rec_start());
         for (int l = 0; l < c.layers; ++l) {
+            bool done = false;
+            LLMI_TRY(rec_layer_fused(l, &done));
+            if (done) continue;
             LLMI_TRY(rec_attn(l));
             if (comm) {  // exact int64 sum of the fixed-point residual partials
                 ncclResult_t r = ncclAllReduce(xacc, xacc, c.hidden, ncclInt64, ncclSum, comm, stream);
                 LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
             }
             LLMI_TRY(rec_ffn(l));
-            LLMI_TRY(allreduce_sum(x, c.hidden));
+            if (comm) {  // exact int64 sum of the layer outputs (rank 0 carried the residual)
+                ncclResult_t r = ncclAllReduce(res[(l + 1) % 2], res[(l + 1) % 2], c.hidden, ncclInt64, ncclSum,
+                                               comm, stream);
+                LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
+            }
         }
         LLMI_TRY(rec_head());
         if (comm) {
@@ -548,7 +613,7 @@ struct Engine {
             }
             if (p0 + m == p_begin + n) {  // last row -> final norm + lm_head + argmax keys
                 LLMI_HIP(hipMemcpyAsync(x, pf_x + (size_t)(m - 1) * H, (size_t)H * 4, hipMemcpyDeviceToDevice, stream));
-                LLMI_TRY(gemv_launch(lm_args(), stream));
+                LLMI_TRY(gemv_launch(lm_args(true), stream));
             }
         }
         LLMI_TRY(prefill_finish_launch(st, prompt, tokens, p_begin, n, stream));
@@ -565,7 +630,8 @@ struct Engine {
         LLMI_HIP(hipStreamSynchronize(stream));
         DecodeState h;
         LLMI_HIP(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
-        LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error));
+        LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error) +
+                                       " (1: token id out of range, 2: position overflow, 4: dataflow wait timed out)");
         const int m = n < valid ? n : valid;
         if (m > 0) LLMI_HIP(hipMemcpy(out, tokens, (size_t)m * 4, hipMemcpyDeviceToHost));
         if (n_valid) *n_valid = valid;
@@ -582,7 +648,7 @@ struct Engine {
 struct Group {
     std::vector<std::unique_ptr<Engine>> r;
     hipStream_t stream = nullptr;
-    void** ptrs = nullptr;  // device [3][W]: xacc, x, partials of every rank
+    void** ptrs = nullptr;  // device [4][W]: xacc, res[0], res[1], partials of every rank
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
 
@@ -605,11 +671,12 @@ struct Group {
             r.emplace_back(new Engine());
             LLMI_TRY(r.back()->init(c, dev, nullptr, stream));
         }
-        std::vector<void*> h(3 * world);
+        std::vector<void*> h(4 * world);
         for (int i = 0; i < world; ++i) {
             h[i] = r[i]->xacc;
-            h[world + i] = r[i]->x;
-            h[2 * world + i] = r[i]->partials;
+            h[world + i] = r[i]->res[0];
+            h[2 * world + i] = r[i]->res[1];
+            h[3 * world + i] = r[i]->partials;
         }
         LLMI_HIP(hipMalloc(&ptrs, h.size() * sizeof(void*)));
         LLMI_HIP(hipMemcpy(ptrs, h.data(), h.size() * sizeof(void*), hipMemcpyHostToDevice));
@@ -623,10 +690,10 @@ struct Group {
             for (auto& e : r) LLMI_TRY(e->rec_attn(l));
             if (W > 1) LLMI_TRY(group_reduce_launch(ptrs, W, H, 0, stream));
             for (auto& e : r) LLMI_TRY(e->rec_ffn(l));
-            if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + W, W, H, 1, stream));
+            if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + (1 + (l + 1) % 2) * W, W, H, 0, stream));
         }
         for (auto& e : r) LLMI_TRY(e->rec_head());
-        if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + 2 * W, W, r[0]->lm_grid, 2, stream));
+        if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + 3 * W, W, r[0]->lm_grid, 2, stream));
         return LLMI_OK;
     }
 
@@ -809,6 +876,37 @@ int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes
 
 llmi_stream_t llmi_engine_stream(llmi_engine* e) { return e ? (llmi_stream_t)e->e.stream : nullptr; }
 
+int llmi_engine_layer_stamps(llmi_engine* e, uint64_t* out, int max_wg, int* n_wg, int* phase_wgs) {
+    LLMI_REQUIRE(e && out && n_wg && phase_wgs, "layer_stamps: null argument");
+    Engine& g = e->e;
+    LLMI_HIP(hipSetDevice(g.device));
+    LLMI_REQUIRE(g.fused, "layer_stamps: the dataflow layer is not in use for this engine");
+    LLMI_REQUIRE(g.prompt_len > 0 && g.host_next_pos > 0, "layer_stamps: decode at least one step first");
+    llmi::LayerArgs L = g.layer_args(0);
+    const size_t cap = (size_t)max_wg * 3 * 8;
+    unsigned long long* dst = nullptr;
+    LLMI_HIP(hipMalloc(&dst, cap));
+    LLMI_HIP(hipMemsetAsync(dst, 0, cap, g.stream));
+    std::vector<char> save((size_t)g.c.hidden * 4);
+    LLMI_HIP(hipMemcpyAsync(save.data(), g.x, save.size(), hipMemcpyDeviceToHost, g.stream));
+    int rc = LLMI_OK;
+    for (int it = 0; it < 3 && rc == LLMI_OK; ++it) {  // the last of three launches is recorded
+        LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
+        L.stamps = (it == 2) ? dst : nullptr;
+        rc = llmi::layer_launch_probe(L, g.stream, max_wg, phase_wgs);
+    }
+    if (rc == LLMI_OK) {
+        LLMI_HIP(hipStreamSynchronize(g.stream));
+        int total = 0;
+        for (int p = 0; p < 5; ++p) total += phase_wgs[p];
+        *n_wg = total;
+        LLMI_HIP(hipMemcpy(out, dst, (size_t)std::min(total, max_wg) * 3 * 8, hipMemcpyDeviceToHost));
+    }
+    (void)hipFree(dst);
+    LLMI_HIP(hipMemcpy(g.x, save.data(), save.size(), hipMemcpyHostToDevice));
+    return rc;
+}
+
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes) {
     LLMI_REQUIRE(e && avg_us && iters > 0, "time_kernel: bad arguments");
     Engine& g = e->e;
@@ -824,8 +922,12 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             case 3: return llmi::gemv_launch(g.gu_args(0), g.stream);
             case 4: return llmi::gemv_launch(g.down_args(0), g.stream);
             case 5: return llmi::gemv_launch(g.lm_args(), g.stream);
+            case 6: {  // dataflow layer 0 (counters re-zeroed per launch)
+                LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
+                return llmi::layer_launch(g.layer_args(0), g.stream);
+            }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..5");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..6");
     };
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
@@ -841,11 +943,23 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
         case 3: b = (uint64_t)2 * g.il * H * ws + 2 * g.il * sc; break;
         case 4: b = (uint64_t)H * g.il * ws + H * sc; break;
         case 5: b = (uint64_t)g.vl * H * g.esz; break;
+        case 6: {
+            LLMI_REQUIRE(g.fused, "time_kernel: the dataflow layer is not in use for this engine");
+            llmi::DecodeState hs;
+            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
+            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
+            b = (g.stream_bytes - (uint64_t)g.vl * H * g.esz - 2 * H * g.esz) / g.c.layers +
+                (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb;
+            break;
+        }
     }
     // timing launches modify the residual stream (o/down epilogues add into x),
     // so save and restore the small activation state around them
-    std::vector<char> save(H * 4);
+    std::vector<char> save(H * 4), save_fx(3 * H * 8);
     LLMI_HIP(hipMemcpyAsync(save.data(), g.x, H * 4, hipMemcpyDeviceToHost, g.stream));
+    long long* fx[3] = {g.xacc, g.res[0], g.res[1]};
+    for (int i = 0; i < 3; ++i)
+        LLMI_HIP(hipMemcpyAsync(save_fx.data() + i * H * 8, fx[i], H * 8, hipMemcpyDeviceToHost, g.stream));
     LLMI_TRY(launch());  // warm
     hipEvent_t t0, t1;
     LLMI_HIP(hipEventCreate(&t0));
@@ -859,6 +973,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
     LLMI_HIP(hipMemcpy(g.x, save.data(), H * 4, hipMemcpyHostToDevice));
+    for (int i = 0; i < 3; ++i) LLMI_HIP(hipMemcpy(fx[i], save_fx.data() + i * H * 8, H * 8, hipMemcpyHostToDevice));
     *avg_us = ms * 1000.f / iters;
     if (bytes) *bytes = b;
     return LLMI_OK;

@@ -1,0 +1,303 @@
+// GEMV body shared by the standalone gemv_kernel (gemv.hip) and the dataflow
+// layer kernel (layer.hip). See gemv.hip for the design notes; IO selects plain
+// or write-through (sc1) access for the activation bytes another workgroup of
+// the same launch produces or consumes, SYNC the dataflow wait/publish.
+#pragma once
+#include "handoff.h"
+#include "kernels.h"
+
+namespace llmi {
+namespace gemv_detail {
+
+constexpr int kThreads = 256;
+constexpr int kWavesPerBlock = kThreads / kWave;
+#ifndef LLMI_GEMV_UNROLL
+#define LLMI_GEMV_UNROLL 8
+#endif
+#ifndef LLMI_GEMV_ROWS
+#define LLMI_GEMV_ROWS 2
+#endif
+constexpr int kUnrollMax = LLMI_GEMV_UNROLL;  // 16-B loads per row in flight per lane
+constexpr int kRows = LLMI_GEMV_ROWS;      // rows per wave (EPI_SILU_MUL always pairs 2)
+
+template <typename WT> struct WT_ { };
+template <> struct WT_<__half> { static constexpr int EPL = 8; };
+template <> struct WT_<float> { static constexpr int EPL = 4; };
+template <> struct WT_<int8_t> { static constexpr int EPL = 16; };
+
+__device__ __forceinline__ float dot_packet(const uint4& w, const float4* xp, int nc, __half*) {
+    const __half2* h = reinterpret_cast<const __half2*>(&w);
+    float4 x0 = xp[0], x1 = xp[nc];
+    float2 a = __half22float2(h[0]), b = __half22float2(h[1]);
+    float2 c = __half22float2(h[2]), d = __half22float2(h[3]);
+    float s = a.x * x0.x;
+    s = fmaf(a.y, x0.y, s);
+    s = fmaf(b.x, x0.z, s);
+    s = fmaf(b.y, x0.w, s);
+    s = fmaf(c.x, x1.x, s);
+    s = fmaf(c.y, x1.y, s);
+    s = fmaf(d.x, x1.z, s);
+    s = fmaf(d.y, x1.w, s);
+    return s;
+}
+__device__ __forceinline__ float dot_packet(const uint4& w, const float4* xp, int nc, float*) {
+    float4 x0 = xp[0];
+    float s = __uint_as_float(w.x) * x0.x;
+    s = fmaf(__uint_as_float(w.y), x0.y, s);
+    s = fmaf(__uint_as_float(w.z), x0.z, s);
+    s = fmaf(__uint_as_float(w.w), x0.w, s);
+    return s;
+}
+__device__ __forceinline__ float i8(uint32_t v, int j) { return (float)(int8_t)((v >> (8 * j)) & 0xff); }
+__device__ __forceinline__ float dot_packet(const uint4& w, const float4* xp, int nc, int8_t*) {
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        float4 x = xp[p * nc];
+        s = fmaf(i8(ws[p], 0), x.x, s);
+        s = fmaf(i8(ws[p], 1), x.y, s);
+        s = fmaf(i8(ws[p], 2), x.z, s);
+        s = fmaf(i8(ws[p], 3), x.w, s);
+    }
+    return s;
+}
+
+__device__ __forceinline__ float silu(float v) { return v / (1.0f + expf(-v)); }
+
+template <typename GT>
+__device__ __forceinline__ float4 gamma4(const void* g, int j) {
+    if constexpr (sizeof(GT) == 2) {
+        const uint2 u = reinterpret_cast<const uint2*>(g)[j];
+        const float2 a = __half22float2(*reinterpret_cast<const __half2*>(&u.x));
+        const float2 b = __half22float2(*reinterpret_cast<const __half2*>(&u.y));
+        return make_float4(a.x, a.y, b.x, b.y);
+    } else {
+        return reinterpret_cast<const float4*>(g)[j];
+    }
+}
+
+// LDS bytes the body needs for a k-wide x: [PK][nc] float4 image + reduction scratch + keys
+__host__ __device__ inline size_t gemv_lds_bytes(int k) { return (size_t)k * 4 + 16 * 4 + kWavesPerBlock * 8; }
+
+// XPT: float4s of x each thread holds in registers during staging (k <= XPT*4*256);
+// 0 = generic strided staging (standalone only).
+// bid / nblk: this workgroup's index in the GEMV grid and the grid size.
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, typename IO,
+          typename SYNC>
+__device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, float4* xs, const SYNC& sync) {
+    // residual hand-over (seed_dst <- seed_src slice); in the dataflow kernel seed_src
+    // is the previous phase's output, so it runs after the wait (below)
+    auto seed = [&, bid0 = bid, nblk0 = nblk]() {
+        if (a.seed_dst == nullptr) return;
+        const int per = (a.seed_n + nblk0 - 1) / nblk0;
+        const int i0 = bid0 * per, i1 = min(i0 + per, a.seed_n);
+        for (int i = i0 + (int)threadIdx.x; i < i1; i += kThreads)
+            IO::st_ll(a.seed_dst + i, a.seed_keep ? IO::ld_ll(a.seed_src + i) : 0ll);
+    };
+    static_assert(!SYNC::kFlow || XPT > 0, "dataflow GEMV needs register x staging");
+    constexpr int EPL = WT_<WT>::EPL;
+    constexpr int PK = EPL / 4;                 // float4 packets per 16-B weight load
+    static_assert(!(XFIX && EPI == EPI_ATOMIC), "split-K reads an fp32 x");
+    // split-K (EPI_ATOMIC): workgroup bid takes K slice bid % S of row-group block bid / S
+    const int S = (EPI == EPI_ATOMIC) ? a.ksplit : 1;
+    const int ks = bid % S;
+    bid /= S;
+    nblk /= S;
+    const int k = a.k / S;                      // this workgroup's K extent
+    const int k4 = k / 4;
+    const int nc = k / EPL;                     // 16-B chunks per row
+    float* red = reinterpret_cast<float*>(xs + k4);
+    unsigned long long* best_s = reinterpret_cast<unsigned long long*>(red + 16);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_groups = (EPI == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + ROWS - 1) / ROWS;
+    const size_t row_bytes = (size_t)(a.ldw ? a.ldw : a.k) * sizeof(WT);
+    const char* wbase = reinterpret_cast<const char*>(a.w) + (size_t)ks * k * sizeof(WT);
+    const float4* x4 = reinterpret_cast<const float4*>(a.x + (size_t)ks * k);
+
+    auto rows_of = [&](int g, int* rows) {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) rows[r] = (EPI == EPI_SILU_MUL) ? g + r * a.pair_off : g * ROWS + r;
+    };
+    // Branch-free streaming: every lane always issues its ROWS x kUnroll loads; out of
+    // range chunks/rows are clamped to a valid address and zeroed by a mask. A
+    // predicated load makes hipcc branch around each load and wait vmcnt(0) per load
+    // (cdna_hip_programming.md §5 "three .s-level traps" (c)), serialising the stream.
+    auto load_batch = [&](uint4 (&wv)[ROWS][kUnroll], const int* rows, int base) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int c = base + u * kWave + lane;
+            const int cc = c < nc ? c : nc - 1;
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                const int rr = rows[r] < a.n_rows ? rows[r] : a.n_rows - 1;
+                const unsigned m = (c < nc && rows[r] < a.n_rows) ? 0xFFFFFFFFu : 0u;
+                uint4 v = ld_nt16(wbase + (size_t)rr * row_bytes + (size_t)cc * 16);
+                v.x &= m; v.y &= m; v.z &= m; v.w &= m;
+                wv[r][u] = v;
+            }
+        }
+    };
+    auto dot_batch = [&](const uint4 (&wv)[ROWS][kUnroll], int base, float* acc) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int c = base + u * kWave + lane;
+            const float4* xp = xs + (c < nc ? c : nc - 1);  // masked chunks have zero weights
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) acc[r] += dot_packet(wv[r][u], xp, nc, (WT*)nullptr);
+        }
+    };
+
+    // ---- prologue. Issue order matters: vmcnt retires loads in issue order, so x
+    // (and gamma) go first, then this wave's first weight batch; the weight stream is
+    // then in flight while x is staged and the norm is reduced. In the dataflow kernel
+    // the weight batch goes first instead (it does not depend on the previous phase)
+    // and x is loaded after the wait.
+    const int g0 = bid * kWavesPerBlock + wave;
+    int rows0[ROWS];
+    rows_of(g0, rows0);
+    uint4 w0[ROWS][kUnroll];
+    float ss = 0.f;
+    const bool wb = XFIX && bid == 0 && a.x_out != nullptr;  // one block writes x back
+    if constexpr (XPT > 0) {
+        // branch-free: clamp the index, load, and predicate only the LDS store
+        float4 xv[XPT], gv[XPT];
+        longlong2 xf[XFIX ? XPT : 1][2];
+        if constexpr (SYNC::kFlow) {
+            load_batch(w0, rows0, 0);
+            sync.wait();
+        }
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            int j = tid + i * kThreads;
+            j = j < k4 ? j : k4 - 1;
+            if constexpr (XFIX) {
+                xf[i][0] = IO::ld_ll2(reinterpret_cast<const longlong2*>(a.x_fixed) + 2 * j);
+                xf[i][1] = IO::ld_ll2(reinterpret_cast<const longlong2*>(a.x_fixed) + 2 * j + 1);
+            } else {
+                xv[i] = IO::ld4(x4 + j);
+            }
+            if (NORM) gv[i] = gamma4<GT>(a.gamma, j);
+        }
+        if constexpr (!SYNC::kFlow) load_batch(w0, rows0, 0);
+        // RMSNorm (modeling_llama.py:112-117) as gamma*x staged + one scalar rsqrt per
+        // dot product in the epilogue: sum_k W[r,k] gamma_k x_k * rstd.
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int j = tid + i * kThreads;
+            if (j < k4) {
+                float4 v;
+                if constexpr (XFIX) {
+                    v = make_float4(from_fixed(xf[i][0].x), from_fixed(xf[i][0].y),
+                                    from_fixed(xf[i][1].x), from_fixed(xf[i][1].y));
+                    if (wb) IO::st4(reinterpret_cast<float4*>(a.x_out) + j, v);
+                } else {
+                    v = xv[i];
+                }
+                if (NORM) {
+                    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                    v.x *= gv[i].x; v.y *= gv[i].y; v.z *= gv[i].z; v.w *= gv[i].w;
+                }
+                xs[(j % PK) * nc + j / PK] = v;
+            }
+        }
+    } else {
+        for (int j = tid; j < k4; j += kThreads) {
+            float4 v;
+            if constexpr (XFIX) {
+                const long long* f = a.x_fixed + 4 * j;
+                v = make_float4(from_fixed(f[0]), from_fixed(f[1]), from_fixed(f[2]), from_fixed(f[3]));
+                if (wb) reinterpret_cast<float4*>(a.x_out)[j] = v;
+            } else {
+                v = x4[j];
+            }
+            if (NORM) {
+                const float4 gg = gamma4<GT>(a.gamma, j);
+                ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                v.x *= gg.x; v.y *= gg.y; v.z *= gg.z; v.w *= gg.w;
+            }
+            xs[(j % PK) * nc + j / PK] = v;
+        }
+        load_batch(w0, rows0, 0);
+    }
+    seed();
+    float rstd = 1.f;
+    if (NORM) {
+        ss = block_sum(ss, red);  // its barriers also publish xs
+        rstd = 1.0f / sqrtf(ss / (float)k + a.eps);
+    } else {
+        __syncthreads();
+    }
+
+    unsigned long long best = 0ull;
+    auto finish = [&](int g, const int* rows, float* acc) {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            acc[r] = wave_sum(acc[r]) * rstd;
+            if (a.scales != nullptr && rows[r] < a.n_rows) acc[r] *= __half2float(a.scales[rows[r]]);
+        }
+        if (EPI == EPI_SILU_MUL) {
+            if (lane == 0) IO::st(a.y + g, silu(acc[0]) * acc[1]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                const int row = rows[r];
+                if (row >= a.n_rows) continue;
+                if (lane == r) {
+                    float v = acc[r];
+                    if (EPI == EPI_ATOMIC) {
+                        atomicAdd(reinterpret_cast<unsigned long long*>(a.yacc + row),
+                                  (unsigned long long)to_fixed(v));
+                    } else {
+                        if (EPI == EPI_ADD) v += a.resid_scale * IO::ld(a.resid + row);
+                        IO::st(a.y + row, v);
+                    }
+                }
+                if (EPI == EPI_ARGMAX) {
+                    unsigned long long kk = argmax_key(acc[r], a.idx_base + (uint32_t)row);
+                    best = kk > best ? kk : best;
+                }
+            }
+        }
+    };
+
+    // ---- first group (its first batch is already in flight)
+    if (g0 < n_groups) {
+        float acc[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+        dot_batch(w0, 0, acc);
+        for (int base = kWave * kUnroll; base < nc; base += kWave * kUnroll) {
+            uint4 wv[ROWS][kUnroll];
+            load_batch(wv, rows0, base);
+            dot_batch(wv, base, acc);
+        }
+        finish(g0, rows0, acc);
+    }
+    // ---- remaining groups
+    for (int g = g0 + nblk * kWavesPerBlock; g < n_groups; g += nblk * kWavesPerBlock) {
+        int rows[ROWS];
+        rows_of(g, rows);
+        float acc[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+        for (int base = 0; base < nc; base += kWave * kUnroll) {
+            uint4 wv[ROWS][kUnroll];
+            load_batch(wv, rows, base);
+            dot_batch(wv, base, acc);
+        }
+        finish(g, rows, acc);
+    }
+    if (EPI == EPI_ARGMAX) {
+        if (lane == 0) best_s[wave] = best;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long b = best_s[0];
+            for (int i = 1; i < kWavesPerBlock; ++i) b = best_s[i] > b ? best_s[i] : b;
+            a.partials[bid] = b;
+        }
+    }
+}
+
+}  // namespace gemv_detail
+}  // namespace llmi

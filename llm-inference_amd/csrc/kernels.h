@@ -13,6 +13,7 @@ enum GemvEpi : int {
     EPI_ADD = 1,       // y[r] = acc + resid_scale * resid[r]   (resid may alias y)
     EPI_SILU_MUL = 2,  // rows (g, g + pair_off): y[g] = silu(acc0) * acc1
     EPI_ARGMAX = 3,    // y[r] = acc; per-block argmax key -> partials[blockIdx]
+    EPI_ATOMIC = 4,    // yacc[r] += fixed(acc) (int64 2^-32 units; exact, order-independent), split-K
 };
 
 struct GemvArgs {
@@ -37,6 +38,15 @@ struct GemvArgs {
     unsigned long long* partials = nullptr;  // EPI_ARGMAX: [grid]
     uint32_t idx_base = 0;         // EPI_ARGMAX: global index of row 0 (vocab shard)
     int grid = 0;                  // 0 = auto
+    int ldw = 0;                   // row stride of W in elements (0: k)
+    int ksplit = 1;                // EPI_ATOMIC: K split over ksplit workgroups (k % (ksplit * 16 B) == 0)
+    long long* yacc = nullptr;     // EPI_ATOMIC target
+    // residual hand-over: the workgroups copy seed_src[0..seed_n) (or zeros when !seed_keep)
+    // to seed_dst, one slice each (the next fixed-point accumulator's starting value)
+    const long long* seed_src = nullptr;
+    long long* seed_dst = nullptr;
+    int seed_n = 0;
+    int seed_keep = 1;
 };
 
 int gemv_launch(const GemvArgs& a, hipStream_t s);
@@ -103,9 +113,12 @@ struct AttnArgs {
     // 1 (operator API): normalized output in `out` (merge kernel when > 1 split);
     // 0 (engine): split partials only, consumed by attn_oproj_launch
     int direct_out = 1;
-    // engine: seed the fixed-point residual accumulator (see attn_oproj_launch)
+    // engine: seed the fixed-point residual accumulator (see attn_oproj_launch) with
+    // resid_fixed (int64 residual stream; or fixed(resid) when only fp32 is given) on the
+    // rank that carries the residual (resid_scale != 0), zeros elsewhere
     long long* xacc = nullptr;
     const float* resid = nullptr;
+    const long long* resid_fixed = nullptr;
     float resid_scale = 1.f;
     int hidden = 0;
 };
@@ -143,6 +156,30 @@ constexpr int kAttnChunk = 64;     // cached positions per workgroup (split-KV)
 size_t attn_workspace_bytes(int heads, int head_dim, int max_seq);
 int attn_decode_launch(const AttnArgs& a, hipStream_t s);
 
+// ------------------------------------------------ dataflow decode layer
+// One launch per layer: q/k/v GEMV, attention, merge + o_proj, gate_up, down
+// workgroups in phase order with counter hand-offs (layer.hip). nb/ns are set by
+// layer_launch; cnt (layer_cnt_words() u32) must be zero before each launch.
+struct LayerArgs {
+    GemvArgs qkv;
+    AttnArgs attn;
+    OprojArgs o;
+    GemvArgs gu;
+    GemvArgs down;
+    int nb[5] = {0, 0, 0, 0, 0};
+    int ns = 0;
+    unsigned* cnt = nullptr;
+    int* err = nullptr;            // sticky error word (DecodeState::error)
+    unsigned long long* stamps = nullptr;  // debug: 3 x u64 per workgroup (see layer.hip)
+};
+int layer_cnt_words();
+// LLMI_EUNSUPPORTED (nothing launched) when the shape/dtype has no instantiation
+int layer_launch(LayerArgs L, hipStream_t s);
+// same, reporting the per-phase workgroup counts (debug timelines)
+int layer_launch_probe(LayerArgs L, hipStream_t s, int max_wg, int* phase_wgs, int first = 0, int last = 4);
+// only phases first..last (0 q/k/v, 1 attention, 2 merge + o_proj, 3 gate_up, 4 down)
+int layer_launch_phases(LayerArgs L, int first, int last, hipStream_t s);
+
 // ------------------------------------------------------ decode-loop state
 struct DecodeState {
     int next_pos;     // position the next forward will process
@@ -155,9 +192,11 @@ struct DecodeState {
 
 // step start: pick the token for position next_pos (prompt id or argmax of
 // the previous forward's partials), record it, gather its embedding row.
+// Also seeds the int64 residual stream xres = fixed(x) (may be null) and zeroes the
+// dataflow layer counters (cnt, cnt_words u32; may be null).
 int step_start_launch(DecodeState* st, const int32_t* prompt, const unsigned long long* partials,
                       int n_partials, int32_t* tokens, const void* table, int table_dtype, int hidden,
-                      float* x, int max_seq, hipStream_t s);
+                      float* x, long long* xres, int max_seq, unsigned* cnt, int cnt_words, hipStream_t s);
 // after the last forward: tokens[next_pos] = argmax(partials) (no state change)
 int finalize_launch(DecodeState* st, const unsigned long long* partials, int n_partials,
                     int32_t* tokens, int max_seq, hipStream_t s);

@@ -141,8 +141,10 @@ __global__ void argmax_final_kernel(const unsigned long long* partials, int np, 
 // choose the token of position next_pos, record it, gather its embedding.
 template <typename TT>
 __global__ void step_start_kernel(DecodeState* st, const int32_t* prompt, const unsigned long long* partials,
-                                  int np, int32_t* tokens, const TT* table, int hidden, float* x, int max_seq) {
+                                  int np, int32_t* tokens, const TT* table, int hidden, float* x,
+                                  long long* xres, int max_seq, unsigned* cnt, int cnt_words) {
     __shared__ unsigned long long sh[16];
+    for (int i = threadIdx.x; i < cnt_words; i += blockDim.x) cnt[i] = 0u;  // this token's layer counters
     __shared__ int tok_s;
     const int p = st->next_pos;
     if (p >= max_seq) {  // host guards this; keep the state consistent if it does not
@@ -173,7 +175,11 @@ __global__ void step_start_kernel(DecodeState* st, const int32_t* prompt, const 
         st->next_pos = p + 1;
     }
     const TT* row = table + (size_t)tok * hidden;
-    for (int i = threadIdx.x; i < hidden; i += blockDim.x) x[i] = to_f32(row[i]);
+    for (int i = threadIdx.x; i < hidden; i += blockDim.x) {
+        const float v = to_f32(row[i]);
+        x[i] = v;
+        if (xres) xres[i] = to_fixed(v);
+    }
 }
 
 __global__ void finalize_kernel(DecodeState* st, const unsigned long long* partials, int np, int32_t* tokens,
@@ -317,14 +323,14 @@ int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long lon
 }
 
 int step_start_launch(DecodeState* st, const int32_t* prompt, const unsigned long long* partials, int np,
-                      int32_t* tokens, const void* table, int t_dtype, int hidden, float* x, int max_seq,
-                      hipStream_t s) {
+                      int32_t* tokens, const void* table, int t_dtype, int hidden, float* x, long long* xres,
+                      int max_seq, unsigned* cnt, int cnt_words, hipStream_t s) {
     if (t_dtype == LLMI_F16)
         hipLaunchKernelGGL(step_start_kernel<__half>, dim3(1), dim3(1024), 0, s, st, prompt, partials, np, tokens,
-                           (const __half*)table, hidden, x, max_seq);
+                           (const __half*)table, hidden, x, xres, max_seq, cnt, cnt ? cnt_words : 0);
     else
         hipLaunchKernelGGL(step_start_kernel<float>, dim3(1), dim3(1024), 0, s, st, prompt, partials, np, tokens,
-                           (const float*)table, hidden, x, max_seq);
+                           (const float*)table, hidden, x, xres, max_seq, cnt, cnt ? cnt_words : 0);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }
