@@ -13,9 +13,13 @@ N GPUs (config 4: head/FFN row/col shard + RCCL all-reduce); each rank streams
 1/N of the weights, total work is fixed ("strong" scaling).
 
 value = generated tokens / s (whole job). Also reported: HBM roofline of the
-dominant kernel (gate_up GEMV, HIP events on the engine stream), the whole
+dominant kernel (gate_up GEMV, HIP events on the engine stream, launches cycling
+through the 32 layers so the weights stream from HBM as in the loop), the whole
 decode loop's algorithmic HBM fraction, and a CPU baseline (the numpy oracle,
-rank 0 at N = 1 only, bounded sample, scaled to the same unit).
+rank 0 at N = 1 only, bounded sample, scaled to the same unit). At N = 1 two
+side measurements of the other single-GPU configs ride along (never `value`):
+"prefill" (config 3: 512-row prompt, MFMA GEMMs, TFLOP/s vs the 2.5 PF dense
+fp16 peak) and "int8_13b" (config 5: Llama-2-13B-shape W8A16 decode).
 """
 from __future__ import annotations
 
@@ -83,6 +87,69 @@ def pmc_traffic(kernel: str):
         return None, None
 
 
+MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (MI355X_MICROARCH.md; 2:1 sparse figures excluded)
+
+
+def prefill_side(eng, prompt_len: int = 512, reps: int = 3):
+    """Config 3 beside the headline: one 512-row prefill (firstTokenGen) in both
+    GEMM precisions on the already-loaded 7B engine. Algorithmic FLOPs: the four
+    projections 2*M*N*K per layer + causal attention 4*heads*d*M(M+1)/2 + lm_head row."""
+    import llmi
+    from llmi.engine import synth_prompt
+    cfg = eng.cfg
+    m = min(prompt_len, cfg.max_seq - 1)
+    lin = cfg.hidden * (cfg.heads + 2 * cfg.kv_heads) * cfg.head_dim + cfg.hidden * cfg.hidden \
+        + 3 * cfg.hidden * cfg.inter
+    flops = cfg.layers * (2 * m * lin + 4 * cfg.heads * cfg.head_dim * (m * (m + 1) // 2)) \
+        + 2 * cfg.hidden * cfg.vocab
+    ids = synth_prompt(SEED + 1, m, cfg.vocab)
+    out = {"config": f"Llama-2-7B fp16 prefill, {m} rows, batch 1 (BASELINE.json configs[2])",
+           "flops": flops, "peak_tflops": MFMA_F16_PEAK_TFLOPS}
+    for exact in (True, False):
+        best = None
+        for _ in range(reps):
+            eng.set_prompt(ids)
+            eng.sync()
+            t0 = time.perf_counter()
+            eng.prefill(m, exact)
+            eng.sync()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        tf = flops / best / 1e12
+        out["exact" if exact else "fp16_activations"] = {
+            "ms": round(best * 1e3, 3), "tflops": round(tf, 1), "frac_of_peak": round(tf / MFMA_F16_PEAK_TFLOPS, 4),
+            "mfma_work_factor": 2 if exact else 1}
+    return out
+
+
+def int8_side(n_new: int = 256):
+    """Config 5 beside the headline: Llama-2-13B-shape int8 W8A16 single-stream decode."""
+    import llmi
+    from llmi.engine import Engine, preset, synth_prompt
+    cfg = preset("llama2-13b", max_seq=PROMPT + n_new)
+    cfg.weight_dtype, cfg.kv_dtype = llmi.I8, llmi.F16
+    with Engine(cfg) as e:
+        e.load_synthetic(SEED)
+        prompt = synth_prompt(SEED, PROMPT, cfg.vocab)
+        e.generate(prompt, 16)  # warm: graph capture
+        e.set_prompt(prompt)
+        e.sync()
+        t0 = time.perf_counter()
+        e.decode(PROMPT + n_new - 1)
+        e.sync()
+        dt = time.perf_counter() - t0
+        wbytes, kvb = e.bytes_per_token()
+        gu_us, gu_b = e.time_kernel("gate_up", iters=128)
+    n_fwd = PROMPT + n_new - 1
+    total = algorithmic_bytes(wbytes, kvb, n_fwd)
+    return {"config": "Llama-2-13B shape, int8 weights + fp16 row scales (W8A16), fp16 KV, batch 1 "
+                      "(BASELINE.json configs[4])",
+            "tokens_per_s": round(n_new / dt, 2), "forwards": n_fwd, "ctx": f"1..{n_fwd}",
+            "weight_bytes_per_token": wbytes,
+            "loop_GBps": round(total / dt / 1e9, 1), "loop_frac_of_8TBps": round(total / dt / 1e9 / HBM_PEAK_GBS, 4),
+            "gate_up_GBps": round(gu_b / (gu_us * 1e-6) / 1e9, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -90,6 +157,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-seq", type=int, default=MAX_SEQ)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-side", action="store_true", help="skip the prefill / int8-13B side measurements")
     ap.add_argument("--kv", choices=["f16", "f32"], default="f16")
     ap.add_argument("--eager", action="store_true",
                     help="launch kernels eagerly instead of replaying the hipGraph (profiling: rocprofv3 "
@@ -155,10 +223,15 @@ def main():
         consistent = all(o == objs[0] for o in objs)
 
     wbytes, kvb = eng.bytes_per_token()
-    # dominant kernel: gate_up GEMV of layer 0, timed with HIP events on the engine stream
-    gu_us, gu_bytes = eng.time_kernel("gate_up", iters=200)
-    kern = {k: eng.time_kernel(k, iters=100) for k in ("qkv", "attn", "o", "down", "lm_head")}
+    # dominant kernel: gate_up GEMV, timed with HIP events on the engine stream
+    gu_us, gu_bytes = eng.time_kernel("gate_up", iters=256)
+    kern = {k: eng.time_kernel(k, iters=128) for k in ("qkv", "attn", "o", "down", "lm_head")}
+    side = {}
+    if world == 1 and not args.no_side:
+        side["prefill"] = prefill_side(eng, prompt_len=512)
     eng.close()
+    if world == 1 and not args.no_side:
+        side["int8_13b"] = int8_side()
 
     if rank != 0:
         if dist is not None:
@@ -188,7 +261,7 @@ def main():
                    "generated_per_step": gen_per_step, "kv_cache": args.kv,
                    "weights": "fp16, fp32 activations/accumulate",
                    "parallelism": f"tp{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": "gate_up GEMV (rmsnorm+gate_up+silu*mul), layer 0",
+        "roofline": {"bound": "hbm", "kernel": "gate_up GEMV (rmsnorm+gate_up+silu*mul), layers cycled",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes": gu_bytes, "avg_us": round(gu_us, 2),
@@ -201,6 +274,7 @@ def main():
         "kernels_GBps": {"gate_up": round(achieved, 1),
                          **{k: round(v[1] / (v[0] * 1e-6) / 1e9, 1) for k, v in kern.items()}},
         "tp_tokens_consistent": consistent,
+        **side,
     }
     if world == 1 and not args.no_cpu_baseline:
         try:

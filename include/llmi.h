@@ -192,9 +192,11 @@ int llmi_engine_kv_slot(llmi_engine* e, int layer, int pos, int which_v, float* 
 int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes_per_pos);
 /* hipStream_t the engine launches on. */
 llmi_stream_t llmi_engine_stream(llmi_engine* e);
-/* Time `iters` eager launches of one kernel of layer 0 (HIP events on the
- * engine stream). which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head,
- * 6 the whole layer as the dataflow kernel (when the engine uses it).
+/* Time `iters` eager launches of one kernel (HIP events on the engine stream);
+ * launch i runs layer i % layers, so its weights stream from HBM as in decode.
+ * which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head, 6 the whole layer as
+ * the dataflow kernel (when the engine uses it; layer 0), 10..14 / 20..24 one
+ * phase inside the dataflow kernel with / without its hand-off (diagnostics).
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
 /* Debug timeline of one dataflow layer launch (layer 0): per workgroup, in

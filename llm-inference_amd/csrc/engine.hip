@@ -914,20 +914,32 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     LLMI_REQUIRE(g.prompt_len > 0 && g.host_next_pos > 0, "time_kernel: decode at least one step first");
     const size_t H = g.c.hidden;
     uint64_t b = 0;
+    // launch i uses layer i % layers: every launch streams weights (and KV) the
+    // previous launches did not touch, as in the decode loop -- replaying one layer
+    // would serve its weights from the 256 MiB Infinity Cache and read high
+    int li = 0;
     auto launch = [&]() -> int {
+        const int l = li++ % g.c.layers;
         switch (which) {
-            case 0: return llmi::gemv_launch(g.qkv_args(0), g.stream);
-            case 1: return llmi::attn_decode_launch(g.attn_args(0), g.stream);
-            case 2: return llmi::attn_oproj_launch(g.o_args(0), g.stream);
-            case 3: return llmi::gemv_launch(g.gu_args(0), g.stream);
-            case 4: return llmi::gemv_launch(g.down_args(0), g.stream);
+            case 0: return llmi::gemv_launch(g.qkv_args(l), g.stream);
+            case 1: return llmi::attn_decode_launch(g.attn_args(l), g.stream);
+            case 2: return llmi::attn_oproj_launch(g.o_args(l), g.stream);
+            case 3: return llmi::gemv_launch(g.gu_args(l), g.stream);
+            case 4: return llmi::gemv_launch(g.down_args(l), g.stream);
             case 5: return llmi::gemv_launch(g.lm_args(), g.stream);
             case 6: {  // dataflow layer 0 (counters re-zeroed per launch)
                 LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
                 return llmi::layer_launch(g.layer_args(0), g.stream);
             }
+            case 10: case 11: case 12: case 13: case 14:    // one phase inside the dataflow kernel
+            case 20: case 21: case 22: case 23: case 24: {  // ... without the hand-off code
+                LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
+                llmi::LayerArgs L = g.layer_args(0);
+                L.plain_diag = which >= 20;
+                return llmi::layer_launch_phases(L, which % 10, which % 10, g.stream);
+            }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..6");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..6, 10..14 or 20..24");
     };
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
@@ -943,6 +955,8 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
         case 3: b = (uint64_t)2 * g.il * H * ws + 2 * g.il * sc; break;
         case 4: b = (uint64_t)H * g.il * ws + H * sc; break;
         case 5: b = (uint64_t)g.vl * H * g.esz; break;
+        case 10: case 11: case 12: case 13: case 14:
+        case 20: case 21: case 22: case 23: case 24: b = 1; break;  // (bytes: see the standalone kernel)
         case 6: {
             LLMI_REQUIRE(g.fused, "time_kernel: the dataflow layer is not in use for this engine");
             llmi::DecodeState hs;

@@ -171,6 +171,7 @@ struct LayerArgs {
     unsigned* cnt = nullptr;
     int* err = nullptr;            // sticky error word (DecodeState::error)
     unsigned long long* stamps = nullptr;  // debug: 3 x u64 per workgroup (see layer.hip)
+    int plain_diag = 0;            // diagnostic: a one-phase launch without hand-off code
 };
 int layer_cnt_words();
 // LLMI_EUNSUPPORTED (nothing launched) when the shape/dtype has no instantiation

@@ -53,11 +53,24 @@ constexpr int kLayerThreads = 256;
 static_assert(kLayerThreads == gemv_detail::kThreads && kLayerThreads == attn_detail::kThreads,
               "the bodies share one workgroup shape");
 
-template <typename WT, typename KT, int XH, int XI, int NPL, int UQ, int UG, int UD>
+// PLAIN (diagnostic, one phase per launch only): the same bodies with plain
+// loads/stores and no hand-off, to separate the hand-off cost from the bodies'
+// code generation inside this kernel
+template <bool PLAIN, bool LD, bool ST>
+using PhIO = typename std::conditional<PLAIN, MixIO<false, false>, MixIO<LD, ST>>::type;
+struct PlainSync : NoSync {
+    const unsigned* wait_cnt = nullptr;
+    unsigned wait_target = 0;
+    unsigned* pub_cnt = nullptr;
+    int* err = nullptr;
+    unsigned long long* stamp = nullptr;
+};
+
+template <typename WT, typename KT, int XH, int XI, int NPL, int UQ, int UG, int UD, bool PLAIN = false>
 __global__ __launch_bounds__(kLayerThreads, LLMI_LAYER_WAVES) void layer_kernel(LayerArgs L) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     int b = blockIdx.x;
-    FlowSync s;
+    typename std::conditional<PLAIN, PlainSync, FlowSync>::type s;
     s.err = L.err;
     unsigned long long t_start = 0;
     if (L.stamps) {  // debug timeline: {start, wait passed, end} per workgroup (100 MHz clock)
@@ -77,7 +90,7 @@ __global__ __launch_bounds__(kLayerThreads, LLMI_LAYER_WAVES) void layer_kernel(
     auto cnt = [&](int ph) { return L.cnt + ph * kPhaseCntWords; };
     if (b < L.nb[PH_QKV]) {
         s.pub_cnt = cnt(PH_QKV);
-        gemv_body<WT, kRows, EPI_STORE, true, __half, XH, UQ, true, MixIO<false, true>>(L.qkv, b, L.nb[PH_QKV],
+        gemv_body<WT, kRows, EPI_STORE, true, __half, XH, UQ, true, PhIO<PLAIN, false, true>>(L.qkv, b, L.nb[PH_QKV],
                                                                                        smem, s);
         s.publish();
         return;
@@ -87,7 +100,7 @@ __global__ __launch_bounds__(kLayerThreads, LLMI_LAYER_WAVES) void layer_kernel(
         s.wait_cnt = cnt(PH_QKV);
         s.wait_target = L.nb[PH_QKV];
         s.pub_cnt = cnt(PH_ATTN);
-        attn_body<KT, MixIO<true, true>>(L.attn, b % L.attn.heads, b / L.attn.heads, L.ns,
+        attn_body<KT, PhIO<PLAIN, true, true>>(L.attn, b % L.attn.heads, b / L.attn.heads, L.ns,
                                          reinterpret_cast<float*>(smem), s);
         s.publish();
         return;
@@ -97,7 +110,7 @@ __global__ __launch_bounds__(kLayerThreads, LLMI_LAYER_WAVES) void layer_kernel(
         s.wait_cnt = cnt(PH_ATTN);
         s.wait_target = L.nb[PH_ATTN];
         s.pub_cnt = cnt(PH_O);
-        oproj_body<WT, NPL, MixIO<true, true>>(L.o, b % L.o.heads, b / L.o.heads, L.ns,
+        oproj_body<WT, NPL, PhIO<PLAIN, true, true>>(L.o, b % L.o.heads, b / L.o.heads, L.ns,
                                                reinterpret_cast<float*>(smem), s);
         s.publish();
         return;
@@ -107,7 +120,7 @@ __global__ __launch_bounds__(kLayerThreads, LLMI_LAYER_WAVES) void layer_kernel(
         s.wait_cnt = cnt(PH_O);
         s.wait_target = L.nb[PH_O];
         s.pub_cnt = cnt(PH_GU);
-        gemv_body<WT, 2, EPI_SILU_MUL, true, __half, XH, UG, true, MixIO<true, true>>(L.gu, b, L.nb[PH_GU], smem,
+        gemv_body<WT, 2, EPI_SILU_MUL, true, __half, XH, UG, true, PhIO<PLAIN, true, true>>(L.gu, b, L.nb[PH_GU], smem,
                                                                                       s);
         s.publish();
         return;
@@ -118,16 +131,24 @@ __global__ __launch_bounds__(kLayerThreads, LLMI_LAYER_WAVES) void layer_kernel(
         s.wait_target = L.nb[PH_GU];
         s.pub_cnt = cnt(PH_DOWN);
         // split-K, int64 atomics into the layer output (read by the next launch)
-        gemv_body<WT, kRows, EPI_ATOMIC, false, float, XI, UD, false, MixIO<true, false>>(L.down, b, L.nb[PH_DOWN],
+        gemv_body<WT, kRows, EPI_ATOMIC, false, float, XI, UD, false, PhIO<PLAIN, true, false>>(L.down, b, L.nb[PH_DOWN],
                                                                                           smem, s);
     }
 }
 
 template <typename WT, typename KT, int XH, int XI, int NPL, int UQ, int UG, int UD>
 int launch_cfg(const LayerArgs& L, size_t lds, hipStream_t s) {
-    int total = 0;
-    for (int p = 0; p < PH_COUNT; ++p) total += L.nb[p];
-    hipLaunchKernelGGL((layer_kernel<WT, KT, XH, XI, NPL, UQ, UG, UD>), dim3(total), dim3(kLayerThreads), lds, s, L);
+    int total = 0, phases = 0;
+    for (int p = 0; p < PH_COUNT; ++p) {
+        total += L.nb[p];
+        phases += L.nb[p] > 0;
+    }
+    if (L.plain_diag && phases == 1)
+        hipLaunchKernelGGL((layer_kernel<WT, KT, XH, XI, NPL, UQ, UG, UD, true>), dim3(total), dim3(kLayerThreads),
+                           lds, s, L);
+    else
+        hipLaunchKernelGGL((layer_kernel<WT, KT, XH, XI, NPL, UQ, UG, UD>), dim3(total), dim3(kLayerThreads), lds, s,
+                           L);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }

@@ -27,6 +27,8 @@ def main():
         st, ph = e.layer_stamps()
         out["layer_us_timed"] = e.time_kernel("layer", 50)[0]
         out["parts_us"] = {k: e.time_kernel(k, 50)[0] for k in NAMES}
+        out["fused_alone_us"] = {k: e.time_kernel("f_" + k, 50)[0] for k in NAMES}
+        out["fused_alone_plain_us"] = {k: e.time_kernel("p_" + k, 50)[0] for k in NAMES}
     b = 0
     phases = {}
     for name, n in zip(NAMES, ph.tolist()):
