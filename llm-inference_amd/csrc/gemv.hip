@@ -24,86 +24,16 @@
 #include "gemv_impl.h"
 
 namespace llmi {
-namespace {
-
-using namespace gemv_detail;
-
+namespace gemv_detail {
 #ifndef LLMI_GEMV_MAX_GRID
 #define LLMI_GEMV_MAX_GRID 1024
 #endif
-#ifndef LLMI_GEMV_MIN_WAVES
-#define LLMI_GEMV_MIN_WAVES 1  // min waves per SIMD (launch-bounds 2nd arg): caps VGPRs
-#endif
-
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX>
-__global__ __launch_bounds__(kThreads, LLMI_GEMV_MIN_WAVES) void gemv_kernel(GemvArgs a) {
-    // all LDS in one 16-B aligned dynamic region (cdna_hip_programming.md G17):
-    // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
-    extern __shared__ __attribute__((aligned(16))) float4 xs[];
-    gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs, NoSync{});
-}
-
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int U, bool XF>
-int launch_u(const GemvArgs& a, int grid, hipStream_t s) {
-    const int kl = (EPI == EPI_ATOMIC) ? a.k / a.ksplit : a.k;  // x extent one workgroup stages
-    const size_t lds = gemv_lds_bytes(kl);
-    const int k4 = kl / 4;
-    if (k4 <= 4 * kThreads)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 4, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k4 <= 5 * kThreads)  // 13B hidden (5120)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 5, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k4 <= 11 * kThreads)  // 7B inter (11008)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 11, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k4 <= 14 * kThreads)  // 13B inter (13824)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 14, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 0, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    LLMI_HIP(hipGetLastError());
-    return LLMI_OK;
-}
-
-// Loads in flight per wave: measured on MI355X (tools/tune_gemv.sh, profiles/):
-// with many row groups per CU (q/k/v, gate_up) 2 rows x 4 loads per wave win
-// (more waves resident); with few groups (o, down: 2048 pairs; lm_head argmax)
-// 2 rows x 8 loads per wave win.
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT>
-int launch_t(const GemvArgs& a, int grid, hipStream_t s) {
-    const int groups = (EPI == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + ROWS - 1) / ROWS;
-    const bool u4 = EPI != EPI_ARGMAX && groups >= 4096 && groups <= 12288 && kUnrollMax >= 4;
-    if (a.x_fixed) {
-        // the engine's residual stream is int64 fixed point: the normed projections read it
-        if constexpr (NORM && EPI != EPI_ADD && EPI != EPI_ATOMIC) {
-            return u4 ? launch_u<WT, ROWS, EPI, NORM, GT, 4, true>(a, grid, s)
-                      : launch_u<WT, ROWS, EPI, NORM, GT, kUnrollMax, true>(a, grid, s);
-        }
-        LLMI_REQUIRE(false, "gemv: a fixed-point x needs rmsnorm and a store/silu/argmax epilogue");
-    }
-    return u4 ? launch_u<WT, ROWS, EPI, NORM, GT, 4, false>(a, grid, s)
-              : launch_u<WT, ROWS, EPI, NORM, GT, kUnrollMax, false>(a, grid, s);
-}
-
-template <typename WT, int ROWS, int EPI>
-int launch_norm(const GemvArgs& a, int grid, hipStream_t s) {
-    if (a.gamma == nullptr) return launch_t<WT, ROWS, EPI, false, float>(a, grid, s);
-    if (a.g_dtype == LLMI_F16) return launch_t<WT, ROWS, EPI, true, __half>(a, grid, s);
-    if (a.g_dtype == LLMI_F32) return launch_t<WT, ROWS, EPI, true, float>(a, grid, s);
-    LLMI_REQUIRE(false, "gemv: gamma dtype must be f16 or f32");
-}
-
 template <typename WT>
-int launch_epi(const GemvArgs& a, int grid, hipStream_t s) {
-    switch (a.epi) {
-        case EPI_STORE: return launch_norm<WT, kRows, EPI_STORE>(a, grid, s);
-        case EPI_ADD: return launch_norm<WT, kRows, EPI_ADD>(a, grid, s);
-        case EPI_SILU_MUL: return launch_norm<WT, 2, EPI_SILU_MUL>(a, grid, s);
-        case EPI_ARGMAX: return launch_norm<WT, kRows, EPI_ARGMAX>(a, grid, s);
-        case EPI_ATOMIC:
-            LLMI_REQUIRE(a.gamma == nullptr, "gemv: the split-K atomic epilogue takes no rmsnorm");
-            return launch_t<WT, kRows, EPI_ATOMIC, false, float>(a, grid, s);
-    }
-    LLMI_REQUIRE(false, "gemv: bad epilogue");
-}
+int launch_epi(const GemvArgs& a, int grid, hipStream_t s);  // gemv_{f16,f32,i8}.hip
+}  // namespace gemv_detail
 
+namespace {
+using namespace gemv_detail;
 int epl_of(int dt) { return dt == LLMI_F16 ? 8 : dt == LLMI_F32 ? 4 : dt == LLMI_I8 ? 16 : 0; }
 
 }  // namespace

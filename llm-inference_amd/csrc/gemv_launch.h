@@ -1,0 +1,111 @@
+// GEMV launchers (templates) shared by the per-weight-dtype translation units
+// gemv_f16.hip / gemv_f32.hip / gemv_i8.hip, which instantiate launch_epi<WT>
+// (split so the build compiles the dtypes in parallel).
+#pragma once
+#include "gemv_impl.h"
+
+namespace llmi {
+namespace gemv_detail {
+
+
+#ifndef LLMI_GEMV_MAX_GRID
+#define LLMI_GEMV_MAX_GRID 1024
+#endif
+#ifndef LLMI_GEMV_MIN_WAVES
+#define LLMI_GEMV_MIN_WAVES 1  // min waves per SIMD (launch-bounds 2nd arg): caps VGPRs
+#endif
+
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX>
+__global__ __launch_bounds__(kThreads, LLMI_GEMV_MIN_WAVES) void gemv_kernel(GemvArgs a) {
+    // all LDS in one 16-B aligned dynamic region (cdna_hip_programming.md G17):
+    // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
+    extern __shared__ __attribute__((aligned(16))) float4 xs[];
+    gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs, NoSync{});
+}
+
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int U, bool XF>
+int launch_u(const GemvArgs& a, int grid, hipStream_t s) {
+    const int kl = (EPI == EPI_ATOMIC) ? a.k / a.ksplit : a.k;  // x extent one workgroup stages
+    const size_t lds = gemv_lds_bytes(kl);
+    const int k4 = kl / 4;
+    if (k4 <= 4 * kThreads)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 4, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k4 <= 5 * kThreads)  // 13B hidden (5120)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 5, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k4 <= 11 * kThreads)  // 7B inter (11008)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 11, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else if (k4 <= 14 * kThreads)  // 13B inter (13824)
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 14, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 0, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+// Loads in flight per wave: measured on MI355X (tools/tune_gemv.sh, profiles/):
+// with many row groups per CU (q/k/v, gate_up) 2 rows x 4 loads per wave win
+// (more waves resident); with few groups (o, down: 2048 pairs; lm_head argmax)
+// 2 rows x 8 loads per wave win.
+// Unroll (16-B loads per row in flight per lane; a batch covers 64 * U chunks of a
+// row). Preference measured on MI355X (tools/tune_gemv.sh, profiles/): with many
+// row groups per CU (q/k/v, gate_up) U = 4 (more waves resident), otherwise U = 8.
+// A U that pads the row's chunk count to fewer batch slots wins over the
+// preference: masked slots cost load issue and VALU (13B rows: 320 int8 / 640
+// fp16 chunks waste 37.5 % / 25 % of their slots at U = 8, none at U = 5).
+template <typename WT, int EPI>
+int pick_unroll(const GemvArgs& a, int groups) {
+    const int kl = (EPI == EPI_ATOMIC) ? a.k / a.ksplit : a.k;
+    const int nc = kl / WT_<WT>::EPL;
+    auto slots = [&](int u) { const int b = kWave * u; return (nc + b - 1) / b * b; };
+    int best = (EPI != EPI_ARGMAX && groups >= 4096 && groups <= 12288 && kUnrollMax >= 4) ? 4 : kUnrollMax;
+    for (int u : {4, 5, 8})
+        if (u <= kUnrollMax && slots(u) < slots(best)) best = u;
+    return best;
+}
+
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, bool XF>
+int launch_x(const GemvArgs& a, int grid, int u, hipStream_t s) {
+    if (u == 4) return launch_u<WT, ROWS, EPI, NORM, GT, 4, XF>(a, grid, s);
+    if (u == 5) return launch_u<WT, ROWS, EPI, NORM, GT, 5, XF>(a, grid, s);
+    return launch_u<WT, ROWS, EPI, NORM, GT, kUnrollMax, XF>(a, grid, s);
+}
+
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT>
+int launch_t(const GemvArgs& a, int grid, hipStream_t s) {
+    const int groups = (EPI == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + ROWS - 1) / ROWS;
+    const int u = pick_unroll<WT, EPI>(a, groups);
+    if (a.x_fixed) {
+        // the engine's residual stream is int64 fixed point: the normed projections read it
+        if constexpr (NORM && EPI != EPI_ADD && EPI != EPI_ATOMIC) {
+            return launch_x<WT, ROWS, EPI, NORM, GT, true>(a, grid, u, s);
+        }
+        LLMI_REQUIRE(false, "gemv: a fixed-point x needs rmsnorm and a store/silu/argmax epilogue");
+    }
+    return launch_x<WT, ROWS, EPI, NORM, GT, false>(a, grid, u, s);
+}
+
+template <typename WT, int ROWS, int EPI>
+int launch_norm(const GemvArgs& a, int grid, hipStream_t s) {
+    if (a.gamma == nullptr) return launch_t<WT, ROWS, EPI, false, float>(a, grid, s);
+    if (a.g_dtype == LLMI_F16) return launch_t<WT, ROWS, EPI, true, __half>(a, grid, s);
+    if (a.g_dtype == LLMI_F32) return launch_t<WT, ROWS, EPI, true, float>(a, grid, s);
+    LLMI_REQUIRE(false, "gemv: gamma dtype must be f16 or f32");
+}
+
+template <typename WT>
+int launch_epi(const GemvArgs& a, int grid, hipStream_t s) {
+    switch (a.epi) {
+        case EPI_STORE: return launch_norm<WT, kRows, EPI_STORE>(a, grid, s);
+        case EPI_ADD: return launch_norm<WT, kRows, EPI_ADD>(a, grid, s);
+        case EPI_SILU_MUL: return launch_norm<WT, 2, EPI_SILU_MUL>(a, grid, s);
+        case EPI_ARGMAX: return launch_norm<WT, kRows, EPI_ARGMAX>(a, grid, s);
+        case EPI_ATOMIC:
+            LLMI_REQUIRE(a.gamma == nullptr, "gemv: the split-K atomic epilogue takes no rmsnorm");
+            return launch_t<WT, kRows, EPI_ATOMIC, false, float>(a, grid, s);
+    }
+    LLMI_REQUIRE(false, "gemv: bad epilogue");
+}
+
+
+}  // namespace gemv_detail
+}  // namespace llmi
