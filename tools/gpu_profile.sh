@@ -19,7 +19,7 @@ timeout -k 10 300 python3 tools/kernel_probe.py --layers 2 --iters 100 --loop --
 cat $OUT/probe_$TAG.json
 echo "[$(date +%T)] kernel trace"
 rm -rf /tmp/prof_trace
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_trace -o trace --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --eager > $OUT/prof_trace_$TAG.log 2>&1 || { echo "trace failed $?"; tail -20 $OUT/prof_trace_$TAG.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_trace -o trace --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-side --eager > $OUT/prof_trace_$TAG.log 2>&1 || { echo "trace failed $?"; tail -20 $OUT/prof_trace_$TAG.log; exit 1; }
 find /tmp/prof_trace -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats_$TAG.csv \;
 python3 tools/trace_summary.py $(find /tmp/prof_trace -name '*kernel_trace.csv' | head -1) > $OUT/trace_summary_$TAG.json || echo "trace summary failed"
 echo "[$(date +%T)] pmc fetch"
@@ -29,5 +29,15 @@ find /tmp/pmc_f -name '*counter_collection.csv' -exec cp {} $OUT/pmc_fetch_$TAG.
 echo "[$(date +%T)] pmc write"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'gemv_kernel' -d /tmp/pmc_w -o pmc --output-format csv -- python3 tools/kernel_probe.py --ctx 64 --kernels gate_up,qkv,lm_head > $OUT/pmc_write_$TAG.log 2>&1 || { echo "pmc write failed $?"; tail -20 $OUT/pmc_write_$TAG.log; exit 1; }
 find /tmp/pmc_w -name '*counter_collection.csv' -exec cp {} $OUT/pmc_write_$TAG.csv \;
+echo "[$(date +%T)] prefill trace"
+rm -rf /tmp/prof_pf
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_pf -o pf --output-format csv -- python3 tools/prefill_probe.py 512 2 > $OUT/prof_prefill_$TAG.log 2>&1 || { echo "prefill trace failed $?"; tail -20 $OUT/prof_prefill_$TAG.log; exit 1; }
+find /tmp/prof_pf -name '*kernel_stats.csv' -exec cp {} $OUT/prefill_kernel_stats_$TAG.csv \;
+echo "[$(date +%T)] pmc mfma (prefill GEMM)"
+rm -rf /tmp/pmc_m
+timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE --kernel-include-regex 'gemm_kernel' -d /tmp/pmc_m -o pmc --output-format csv -- python3 tools/prefill_probe.py 512 1 > $OUT/pmc_mfma_$TAG.log 2>&1 || { echo "pmc mfma failed $?"; tail -20 $OUT/pmc_mfma_$TAG.log; exit 1; }
+find /tmp/pmc_m -name '*counter_collection.csv' -exec cp {} $OUT/pmc_mfma_$TAG.csv \;
+echo "[$(date +%T)] counters available"
+timeout -k 10 120 rocprofv3 -L > $OUT/rocprof_counters_$TAG.txt 2>&1 || true
 echo "[$(date +%T)] done"
 ls -la $OUT

@@ -24,15 +24,17 @@ def per_kernel(path, counter):
 
 
 def main():
+    if len(sys.argv) != 4:
+        raise SystemExit("usage: pmc_summarize.py <fetch.csv> <write.csv> <out.json>")
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
-    write = per_kernel(sys.argv[2], "WRITE_SIZE") if len(sys.argv) > 3 else {}
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on tools/kernel_probe.py; "
                      "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
            "kernels_raw": {}}
     for k, f in fetch.items():
         w = write.get(k, 0.0)
         out["kernels_raw"][k] = {"fetch_kb": f, "write_kb": w, "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024)}
-    json.dump(out, open(sys.argv[-1], "w"), indent=1)
+    json.dump(out, open(sys.argv[3], "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
