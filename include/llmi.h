@@ -199,6 +199,11 @@ llmi_stream_t llmi_engine_stream(llmi_engine* e);
  * phase inside the dataflow kernel with / without its hand-off (diagnostics).
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
+/* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built
+ * afterwards) write a per-workgroup timeline into dev_buf (8 x uint64 per
+ * workgroup at 8 * linear block id: start, two kernel-defined marks, end, CU id;
+ * 100 MHz clock). NULL switches it off. */
+int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf);
 /* Debug timeline of one dataflow layer launch (layer 0): per workgroup, in
  * dispatch order, {start, wait passed, end} of the 100 MHz s_memrealtime clock
  * (3 x uint64 each, max_wg workgroups); phase_wgs[5] receives the workgroups of

@@ -86,21 +86,29 @@ __device__ __forceinline__ void rope_cs(int pos, int i, int d, float base, float
     *s = (float)sd;
 }
 
+#ifndef LLMI_OPROJ_NOMERGE
+#define LLMI_OPROJ_NOMERGE 0
+#endif
+#ifndef LLMI_OPROJ_NOATOMIC
+#define LLMI_OPROJ_NOATOMIC 0
+#endif
+constexpr int kCntWordsPerHead = 64;  // 256 B: heads' counters never share a line
 struct Ws {
-    unsigned* counters;  // [heads]
+    unsigned* counters;  // [heads][kCntWordsPerHead]: fused attention + o_proj arrivals (word 0) and
+                         // departures (word 1), self-resetting; one 256-B line per head
     float* ml;           // [heads][nsplit][2]
     float* o;            // [heads][nsplit][D]
 };
 __host__ __device__ inline size_t ws_bytes(int heads, int max_seq) {
     const int ns = (max_seq + CH - 1) / CH;
-    size_t c = ((size_t)heads * 4 + 255) / 256 * 256;
+    size_t c = (size_t)heads * kCntWordsPerHead * 4;
     return c + (size_t)heads * ns * 2 * 4 + (size_t)heads * ns * D * 4;
 }
 __device__ inline Ws ws_carve(void* base, int heads, int ns) {
     Ws w;
     char* p = reinterpret_cast<char*>(base);
     w.counters = reinterpret_cast<unsigned*>(p);
-    p += ((size_t)heads * 4 + 255) / 256 * 256;
+    p += (size_t)heads * kCntWordsPerHead * 4;
     w.ml = reinterpret_cast<float*>(p);
     p += (size_t)heads * ns * 2 * 4;
     w.o = reinterpret_cast<float*>(p);
@@ -317,9 +325,25 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
 template <int NPL>
 constexpr size_t oproj_lds() { return (2 * kMaxSplits + 4 + D + 2 * D + 16 * NPL) * sizeof(float); }
 
-template <typename WT, int NPL, typename IO, typename SYNC>
+template <typename WT, int NPL>
+__device__ __forceinline__ void oproj_load_w(const OprojArgs& a, int h, int chunk, W8<WT> (&wr)[NPL]) {
+    const int grp = threadIdx.x / LPR, l16 = threadIdx.x % LPR;
+    const int row0 = chunk * 16 * NPL;
+    const WT* w = reinterpret_cast<const WT*>(a.w);
+#pragma unroll
+    for (int t = 0; t < NPL; ++t) {
+        int row = row0 + grp + 16 * t;
+        row = row < a.n_rows ? row : a.n_rows - 1;
+        const size_t off = a.head_major ? ((size_t)h * a.n_rows + row) * D : (size_t)row * a.ldw + (size_t)h * D;
+        wr[t] = ld_w8<WT>(w + off + l16 * 8);
+    }
+}
+
+// PRE: the W_o slice was issued by the caller (oproj_load_w into *pre) before
+// other work; SYNC::kFlow: wait for the partials' producers after the W_o issue.
+template <typename WT, int NPL, typename IO, typename SYNC, bool PRE = false>
 __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk, int ns, float* smem,
-                                           const SYNC& sync) {
+                                           const SYNC& sync, W8<WT> (*pre)[NPL] = nullptr) {
     float* m_s = smem;
     float* l_s = m_s + kMaxSplits;
     float& linv_s = l_s[kMaxSplits];
@@ -337,31 +361,53 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
     const float* mlh = ws.ml + (size_t)h * ns * 2;
     const float* oh = ws.o + (size_t)h * ns * D + d;
     float ov[kMergeChunk];
-    W8<WT> wr[NPL];
+    W8<WT> wr_own[NPL];
+    W8<WT> (&wr)[NPL] = PRE ? *pre : wr_own;
     auto load_w = [&]() {
-#pragma unroll
-        for (int t = 0; t < NPL; ++t) {
-            int row = row0 + grp + 16 * t;
-            row = row < a.n_rows ? row : a.n_rows - 1;
-            wr[t] = ld_w8<WT>(w + (size_t)row * a.ldw + (size_t)h * D + l16 * 8);
-        }
+        if constexpr (!PRE) oproj_load_w<WT, NPL>(a, h, chunk, wr_own);
     };
-    // issue order: standalone -- partials first (needed first), then the W_o slice;
+    (void)w;
+    // issue order: standalone -- partials first (needed first), then the W_o slice,
+    // all into registers before anything waits (a load stored straight to LDS makes
+    // the compiler wait for it -- and for every load issued before it -- right
+    // there, which had serialised the partials' latency in front of the W_o stream);
     // dataflow -- the W_o slice first (independent of the attention phase), wait, partials
     if constexpr (SYNC::kFlow) {
         load_w();
         sync.wait();
     }
+#if LLMI_OPROJ_NOMERGE  // diagnostic only (wrong output): no partial loads, no merge
+    if (true) {
+        load_w();
+        if (tid < D) o_s[tid] = 1.0f;
+        __syncthreads();
+    } else
+#endif
+    {
 #pragma unroll
     for (int i = 0; i < kMergeChunk; ++i) {
         const int sp = half + 2 * i;
         ov[i] = IO::ld(oh + (size_t)(sp < ns ? sp : 0) * D);
     }
-    for (int sp = tid; sp < ns; sp += kThreads) {
-        m_s[sp] = IO::ld(mlh + 2 * sp);
-        l_s[sp] = IO::ld(mlh + 2 * sp + 1);
+    constexpr int kMlPer = kMaxSplits / kThreads;
+    float mr[kMlPer], lr[kMlPer];
+#pragma unroll
+    for (int i = 0; i < kMlPer; ++i) {
+        if (i * kThreads < ns) {  // uniform branch: no per-lane predication of the loads
+            const int sp = min(tid + i * kThreads, ns - 1);
+            mr[i] = IO::ld(mlh + 2 * sp);
+            lr[i] = IO::ld(mlh + 2 * sp + 1);
+        }
     }
     if constexpr (!SYNC::kFlow) load_w();
+#pragma unroll
+    for (int i = 0; i < kMlPer; ++i) {
+        const int sp = tid + i * kThreads;
+        if (i * kThreads < ns && sp < ns) {
+            m_s[sp] = mr[i];
+            l_s[sp] = lr[i];
+        }
+    }
     if (pos < 0 || pos >= a.max_seq) return;
     const int nact = (pos + 1 + CH - 1) / CH;
     __syncthreads();
@@ -391,6 +437,7 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
     __syncthreads();
     if (tid < D) o_s[tid] = (o_red[0][tid] + o_red[1][tid]) * linv_s;
     __syncthreads();
+    }
 
     float xv[8];
 #pragma unroll
@@ -412,7 +459,11 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
         if (row < a.n_rows) {
             float v = y_s[tid];
             if (a.scales) v *= __half2float(a.scales[row]);
+#if LLMI_OPROJ_NOATOMIC  // diagnostic only (wrong sums): plain store instead of the atomic add
+            a.xacc[row] = to_fixed(v);
+#else
             atomicAdd(reinterpret_cast<unsigned long long*>(a.xacc + row), (unsigned long long)to_fixed(v));
+#endif
         }
     }
 }

@@ -107,4 +107,25 @@ __device__ __forceinline__ uint4 ld_nt16(const void* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Debug timeline (diagnostics only; a null base costs one scalar compare): per
+// workgroup 8 u64 at base + 8 * linear block id: [0] start, [1]/[2] kernel-defined
+// marks, [3] end, [4] __smid() -- 100 MHz s_memrealtime clock.
+struct WgStamp {
+    unsigned long long* p;
+    unsigned long long t0;
+    __device__ __forceinline__ explicit WgStamp(unsigned long long* base)
+        : p(base ? base + 8 * ((size_t)blockIdx.x + (size_t)gridDim.x * blockIdx.y) : nullptr),
+          t0(base ? __builtin_amdgcn_s_memrealtime() : 0ull) {}
+    __device__ __forceinline__ void mark(int i) const {
+        if (p && threadIdx.x == 0) p[i] = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ ~WgStamp() {
+        if (p && threadIdx.x == 0) {
+            p[0] = t0;
+            p[3] = __builtin_amdgcn_s_memrealtime();
+            p[4] = __smid();
+        }
+    }
+};
+
 }  // namespace llmi

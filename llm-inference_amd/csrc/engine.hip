@@ -104,6 +104,7 @@ struct Engine {
     int pf_rows = 0;
     float *pf_x = nullptr, *pf_qkv = nullptr, *pf_o = nullptr, *pf_act = nullptr;
     int host_next_pos = 0, prompt_len = 0;
+    unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
     uint64_t seed = 0;
 
     ~Engine() {  // teardown errors are not actionable; ignore them explicitly
@@ -260,10 +261,16 @@ struct Engine {
         layer_cnt = (unsigned*)(scratch + o_cnt);
         {
             const char* env = std::getenv("LLMI_FUSED");
-            // LLMI_FUSED=1: whole layer (measured slower than the five launches);
-            // LLMI_FUSED=2: attention + o_proj pair
-            fuse_mode = (wdt == LLMI_F32 || !env) ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : 0;
+            // default (0): separate attention and merge/o_proj launches;
+            // LLMI_FUSED=1: whole dataflow layer (measured slower than five launches);
+            // LLMI_FUSED=2: dataflow attention + o_proj phases (measured even);
+            // LLMI_FUSED=3: attention + merge/o_proj co-scheduled per head in one launch
+            //               (attn.hip; measured 21.8 vs 19.8 us for the two launches at ctx 2048)
+            fuse_mode = !env ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : env[0] == '3' ? 3 : 0;
+            if (wdt == LLMI_F32 && (fuse_mode == 1 || fuse_mode == 2)) fuse_mode = 0;
             if (fuse_mode == 1 && (c.tp_world != 1 || grouped)) fuse_mode = 2;
+            if (fuse_mode == 3 && attn_oproj_fused_check(attn_args_fused(0), o_args(0), device) != LLMI_OK)
+                fuse_mode = 0;  // shape unsupported or grid not co-resident: separate launches
             fused = fuse_mode == 1;
             const char* ks = std::getenv("LLMI_DOWN_KSPLIT");
             down_ksplit = ks ? std::max(1, std::atoi(ks)) : (fused ? 4 : 1);
@@ -304,7 +311,11 @@ struct Engine {
             LLMI_TRY(fill(L.qkv, 0, lin, wdt, t(prng::Q), ql, H, r * ql, 0, H));
             LLMI_TRY(fill(L.qkv, ql, lin, wdt, t(prng::K), kvrows, H, r * kvrows, 0, H));
             LLMI_TRY(fill(L.qkv, ql + kvrows, lin, wdt, t(prng::V), kvrows, H, r * kvrows, 0, H));
-            LLMI_TRY(fill(L.o, 0, lin, wdt, t(prng::O), H, ql, 0, r * ql, c.heads * c.head_dim));
+            // W_o head-major, [hl][H][head_dim]: the o_proj workgroup of (head, row chunk)
+            // streams one contiguous slab instead of 256-B row segments 8 KB apart
+            for (int hh = 0; hh < hl; ++hh)
+                LLMI_TRY(fill(L.o, (size_t)hh * H, lin, wdt, t(prng::O), H, c.head_dim, 0, r * ql + hh * c.head_dim,
+                              c.heads * c.head_dim));
             // fused [gate; up] rows (layer_weights.cc:40 order)
             LLMI_TRY(fill(L.gu, 0, lin, wdt, t(prng::GATE), il, H, r * il, 0, H));
             LLMI_TRY(fill(L.gu, il, lin, wdt, t(prng::UP), il, H, r * il, 0, H));
@@ -332,6 +343,7 @@ struct Engine {
     // ---------------------------------------------------------- one token
     GemvArgs lm_args(bool from_x = false) const {
         GemvArgs a;
+        a.stamps = dbg_stamps;
         a.w = lm_head;
         a.w_dtype = edt;
         a.n_rows = vl;
@@ -355,14 +367,25 @@ struct Engine {
     GemvArgs qkv_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
+        a.stamps = dbg_stamps;
         a.w = L.qkv; a.scales = L.qkv_s; a.w_dtype = wdt;
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
+        if (fuse_mode == 3) {  // the fused attention + o_proj adds into xacc from its first workgroup on:
+            a.seed_src = res[l % 2]; a.seed_dst = xacc; a.seed_n = c.hidden;  // seed it here
+            a.seed_keep = c.tp_rank == 0 ? 1 : 0;                               // (rank 0 carries the residual)
+        }
+        return a;
+    }
+    AttnArgs attn_args_fused(int l) const {
+        AttnArgs a = attn_args(l);
+        a.xacc = nullptr;  // seeded by the q/k/v GEMV instead
         return a;
     }
     AttnArgs attn_args(int l) const {
         AttnArgs a;
+        a.stamps = dbg_stamps;
         const size_t eb = dtype_size(c.kv_dtype);
         a.qkv = qkv_buf;
         a.k_cache = (char*)kcache + (size_t)l * kv_layer_elems * eb;
@@ -383,7 +406,9 @@ struct Engine {
     OprojArgs o_args(int l) const {
         const Layer& L = layers[l];
         OprojArgs a;
+        a.stamps = dbg_stamps;
         a.w = L.o; a.scales = L.o_s; a.w_dtype = wdt;
+        a.head_major = 1;
         a.n_rows = c.hidden; a.ldw = ql;
         a.heads = hl; a.head_dim = c.head_dim; a.max_seq = c.max_seq;
         a.pos_dev = &st->cur_pos;
@@ -393,6 +418,7 @@ struct Engine {
     GemvArgs gu_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
+        a.stamps = dbg_stamps;
         a.w = L.gu; a.scales = L.gu_s; a.w_dtype = wdt;
         a.n_rows = 2 * il; a.k = c.hidden;
         a.x_fixed = xacc; a.x_out = x;  // residual after attention, written back to x by workgroup 0
@@ -406,6 +432,7 @@ struct Engine {
     GemvArgs down_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
+        a.stamps = dbg_stamps;
         a.w = L.down; a.scales = L.down_s; a.w_dtype = wdt;
         a.n_rows = c.hidden; a.k = il; a.x = act;
         a.epi = EPI_ATOMIC; a.yacc = res[(l + 1) % 2];
@@ -419,7 +446,7 @@ struct Engine {
     // group (struct Group) can interleave its ranks between the reductions.
     int rec_start() {
         return step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, res[0], c.max_seq,
-                                 fuse_mode ? layer_cnt : nullptr, c.layers * layer_cnt_words(), stream);
+                                 (fuse_mode == 1 || fuse_mode == 2) ? layer_cnt : nullptr, c.layers * layer_cnt_words(), stream);
     }
     LayerArgs layer_args(int l) const {
         LayerArgs L;
@@ -448,6 +475,7 @@ struct Engine {
     }
     int rec_attn(int l) {
         LLMI_TRY(gemv_launch(qkv_args(l), stream));
+        if (fuse_mode == 3) return attn_oproj_fused_launch(attn_args_fused(l), o_args(l), &st->error, stream);
         if (fuse_mode == 2) {
             const int rc = layer_launch_phases(layer_args(l), 1, 2, stream);
             if (rc != LLMI_EUNSUPPORTED) return rc;
@@ -597,9 +625,10 @@ struct Engine {
                 LLMI_TRY(prefill_attn_launch(pa, stream));
                 // o_proj + residual
                 g.a = pf_o; g.lda = ql; g.gamma = nullptr;
-                g.w = L.o; g.scales = L.o_s; g.n = H; g.k = ql;
+                g.w = L.o; g.scales = L.o_s; g.n = H; g.k = ql; g.w_kblock = c.head_dim;  // head-major W_o
                 g.epi = EPI_ADD; g.y = pf_x; g.ldy = H;
                 LLMI_TRY(gemm_launch(g, stream));
+                g.w_kblock = 0;
                 // rmsnorm + gate_up + silu * up
                 g.a = pf_x; g.lda = H; g.gamma = L.ffn_norm;
                 g.w = L.gu; g.scales = L.gu_s; g.n = 2 * il; g.k = H;
@@ -907,6 +936,12 @@ int llmi_engine_layer_stamps(llmi_engine* e, uint64_t* out, int max_wg, int* n_w
     return rc;
 }
 
+int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf) {
+    LLMI_REQUIRE(e, "debug_stamps: null engine");
+    e->e.dbg_stamps = static_cast<unsigned long long*>(dev_buf);
+    return LLMI_OK;
+}
+
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes) {
     LLMI_REQUIRE(e && avg_us && iters > 0, "time_kernel: bad arguments");
     Engine& g = e->e;
@@ -927,6 +962,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             case 3: return llmi::gemv_launch(g.gu_args(l), g.stream);
             case 4: return llmi::gemv_launch(g.down_args(l), g.stream);
             case 5: return llmi::gemv_launch(g.lm_args(), g.stream);
+            case 7: return llmi::attn_oproj_fused_launch(g.attn_args_fused(l), g.o_args(l), &g.st->error, g.stream);
             case 6: {  // dataflow layer 0 (counters re-zeroed per launch)
                 LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
                 return llmi::layer_launch(g.layer_args(0), g.stream);
@@ -939,7 +975,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
                 return llmi::layer_launch_phases(L, which % 10, which % 10, g.stream);
             }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..6, 10..14 or 20..24");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..7, 10..14 or 20..24");
     };
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
@@ -952,6 +988,14 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             break;
         }
         case 2: b = (uint64_t)H * g.ql * ws + H * sc; break;
+        case 7: {  // attention (K/V read + slot write) + W_o
+            llmi::DecodeState hs;
+            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
+            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
+            b = (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb +
+                (uint64_t)H * g.ql * ws + H * sc;
+            break;
+        }
         case 3: b = (uint64_t)2 * g.il * H * ws + 2 * g.il * sc; break;
         case 4: b = (uint64_t)H * g.il * ws + H * sc; break;
         case 5: b = (uint64_t)g.vl * H * g.esz; break;

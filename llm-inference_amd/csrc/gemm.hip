@@ -105,7 +105,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs a) {
         b_row[i] = idx / CPR;
         b_col[i] = (idx % CPR) * B_CHUNK;
         const int src = b_src_row(EPI, n0, b_row[i], a.pair_off);
-        b_src[i] = static_cast<const char*>(a.w) + ((size_t)src * K + b_col[i]) * (WT == LLMI_I8 ? 1 : 2);
+        const size_t ldb = a.w_kblock ? a.w_kblock : K;
+        b_src[i] = static_cast<const char*>(a.w) + ((size_t)src * ldb + b_col[i]) * (WT == LLMI_I8 ? 1 : 2);
     }
 
     f4 ra[A_LOADS];
@@ -115,11 +116,13 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs a) {
     for (int i = 0; i < A_LOADS; ++i) ss[i] = 0.f;
 
     auto load = [&](int k0) {
+        // head-major W: K block k0 / w_kblock is an [n][w_kblock] slab
+        const size_t koff = a.w_kblock ? (size_t)(k0 / a.w_kblock) * a.n * a.w_kblock + k0 % a.w_kblock : (size_t)k0;
 #pragma unroll
         for (int i = 0; i < A_LOADS; ++i) ra[i] = *reinterpret_cast<const f4*>(a_src[i] + k0);
 #pragma unroll
         for (int i = 0; i < B_LOADS; ++i)
-            rb[i] = *reinterpret_cast<const u32x4*>(b_src[i] + (size_t)k0 * (WT == LLMI_I8 ? 1 : 2));
+            rb[i] = *reinterpret_cast<const u32x4*>(b_src[i] + koff * (WT == LLMI_I8 ? 1 : 2));
     };
     auto stage = [&](int k0) {
         f4 g = f4{1.f, 1.f, 1.f, 1.f};
@@ -294,6 +297,8 @@ int gemm_launch(GemmArgs a, hipStream_t s) {
     LLMI_REQUIRE(a.lda % 4 == 0 && (reinterpret_cast<uintptr_t>(a.a) & 15) == 0, "gemm: A rows must be 16-B aligned");
     LLMI_REQUIRE((reinterpret_cast<uintptr_t>(a.w) & 15) == 0, "gemm: W must be 16-B aligned");
     LLMI_REQUIRE(a.split == 1 || a.split == 2, "gemm: split must be 1 or 2");
+    LLMI_REQUIRE(a.w_kblock == 0 || (a.w_kblock % kBK == 0 && a.k % a.w_kblock == 0 && a.epi != EPI_SILU_MUL),
+                 "gemm: w_kblock must be a multiple of 64 dividing K (not with the gate_up pairing)");
     LLMI_REQUIRE(a.epi != EPI_SILU_MUL || a.pair_off == a.n / 2, "gemm: gate_up pair offset must be N / 2");
     const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
     a.n_tiles = ncols / ((a.epi == EPI_SILU_MUL) ? kBN / 2 : kBN);

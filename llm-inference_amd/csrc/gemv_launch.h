@@ -20,6 +20,7 @@ __global__ __launch_bounds__(kThreads, LLMI_GEMV_MIN_WAVES) void gemv_kernel(Gem
     // all LDS in one 16-B aligned dynamic region (cdna_hip_programming.md G17):
     // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
+    WgStamp ts(a.stamps);
     gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs, NoSync{});
 }
 

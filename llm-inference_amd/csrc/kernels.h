@@ -17,6 +17,7 @@ enum GemvEpi : int {
 };
 
 struct GemvArgs {
+    unsigned long long* stamps = nullptr;  // debug timeline (WgStamp), null = off
     const void* w = nullptr;       // [n_rows, k] row-major, dtype w_dtype
     const __half* scales = nullptr;  // int8: per-row fp16 scale
     int w_dtype = LLMI_F16;
@@ -61,6 +62,7 @@ struct GemmArgs {
     int g_dtype = LLMI_F16;
     float eps = 1e-5f;
     const void* w = nullptr;       // [n, k] fp16 or int8
+    int w_kblock = 0;              // > 0: W stored as [k / w_kblock][n][w_kblock] (head-major W_o)
     const __half* scales = nullptr;  // int8: per-row fp16 scale
     int w_dtype = LLMI_F16;
     int m = 0, n = 0, k = 0;
@@ -97,6 +99,7 @@ int prefill_finish_launch(struct DecodeState* st, const int32_t* prompt, int32_t
 
 // ------------------------------------------------------------- attention
 struct AttnArgs {
+    unsigned long long* stamps = nullptr;  // debug timeline (WgStamp), null = off
     const float* qkv = nullptr;    // [(heads + 2 kv_heads) * D]
     void* k_cache = nullptr;       // layer base: [kv_heads, max_seq, D]
     void* v_cache = nullptr;
@@ -128,8 +131,10 @@ struct AttnArgs {
 // xacc[rows] with int64 fixed-point atomics (exact, so the sum is independent of
 // arrival order: deterministic). xacc was seeded by the attention kernel.
 struct OprojArgs {
-    const void* w = nullptr;        // W_o (rank shard): [n_rows, ldw] row-major
+    unsigned long long* stamps = nullptr;  // debug timeline (WgStamp), null = off
+    const void* w = nullptr;        // W_o (rank shard): [n_rows, ldw] row-major, or head-major
     const __half* scales = nullptr; // int8 per-row scales
+    int head_major = 0;             // 1: w is [heads][n_rows][head_dim] (each head's slice contiguous)
     int w_dtype = LLMI_F16;
     int n_rows = 0, ldw = 0;
     int heads = 0, head_dim = 128;
@@ -140,6 +145,11 @@ struct OprojArgs {
     long long* xacc = nullptr;
 };
 int attn_oproj_launch(const OprojArgs& a, hipStream_t s);
+// attention + merge/o_proj as one launch (attn.hip); aa.xacc must be null (the
+// residual seed moves to the q/k/v GEMV) and aa.direct_out 0. _check returns
+// LLMI_OK when the shape is supported and the whole grid is co-resident on `device`.
+int attn_oproj_fused_check(const AttnArgs& aa, const OprojArgs& oa, int device);
+int attn_oproj_fused_launch(const AttnArgs& aa, const OprojArgs& oa, int* err, hipStream_t s);
 
 // fixed-point residual accumulator: value = int64 * 2^-32
 __host__ __device__ __forceinline__ long long to_fixed(float v) {

@@ -1,6 +1,6 @@
-"""Dataflow layer kernel (layer.hip) on the MI355X: one launch per layer with
-in-launch counter hand-offs must produce exactly what the five standalone
-launches produce -- same device bodies, same arithmetic, and the o_proj's
+"""Dataflow layer kernel (layer.hip, LLMI_FUSED=1) and the co-scheduled
+attention + o_proj launch (attn.hip, LLMI_FUSED=3) on the MI355X: in-launch
+counter hand-offs must produce exactly what the standalone launches produce -- same device bodies, same arithmetic, and the o_proj's
 int64 fixed-point atomics are order-independent -- so the bar is bitwise
 equality of tokens and logits, plus the reference fixtures as usual."""
 import os
@@ -23,7 +23,7 @@ def rel(a, b):
 
 def run(cfg, seed, prompt, n_new, fused, use_graph=True):
     old = os.environ.get("LLMI_FUSED")
-    os.environ["LLMI_FUSED"] = "1" if fused else "0"
+    os.environ["LLMI_FUSED"] = fused if isinstance(fused, str) else ("1" if fused else "0")
     os.environ["LLMI_DOWN_KSPLIT"] = "4"  # both paths run the same down slicing (bitwise comparison)
     try:
         with Engine(cfg) as e:
@@ -38,18 +38,19 @@ def run(cfg, seed, prompt, n_new, fused, use_graph=True):
             os.environ["LLMI_FUSED"] = old
 
 
+@pytest.mark.parametrize("mode", ["1", "3"])
 @pytest.mark.parametrize("name,cfgname,over,wdt,kv", [
     ("tiny.npz", "tiny", {}, _lib.F16, _lib.F32),
     ("f3_decode.npz", "llama2-7b", dict(layers=2, max_seq=64), _lib.F16, _lib.F32),
     ("f3_decode.npz", "llama2-7b", dict(layers=2, max_seq=64), _lib.F16, _lib.F16),
     ("f5_int8.npz", "llama2-13b", dict(layers=1, max_seq=32), _lib.I8, _lib.F32),
 ])
-def test_fused_equals_unfused_bitwise(name, cfgname, over, wdt, kv):
+def test_fused_equals_unfused_bitwise(name, cfgname, over, wdt, kv, mode):
     f = np.load(os.path.join(G, name))
     cfg = preset(cfgname, **over)
     cfg.weight_dtype, cfg.kv_dtype = wdt, kv
     n = len(f["tokens"])
-    tf, lf, hf = run(cfg, int(f["seed"]), f["prompt"], n, True)
+    tf, lf, hf = run(cfg, int(f["seed"]), f["prompt"], n, mode)
     tu, lu, hu = run(cfg, int(f["seed"]), f["prompt"], n, False)
     np.testing.assert_array_equal(tf, tu)
     np.testing.assert_array_equal(lf, lu)
@@ -61,13 +62,14 @@ def test_fused_equals_unfused_bitwise(name, cfgname, over, wdt, kv):
         assert r < 1e-3
 
 
-def test_fused_full_7b_long_context_bitwise():
+@pytest.mark.parametrize("mode", ["1", "3"])
+def test_fused_full_7b_long_context_bitwise(mode):
     """Bench model past many split-KV chunks: 300 forwards, graph replay and eager."""
     cfg = preset("llama2-7b", max_seq=512)
     prompt = synth_prompt(0, 8, cfg.vocab)
-    tf, lf, _ = run(cfg, 0, prompt, 300, True)
+    tf, lf, _ = run(cfg, 0, prompt, 300, mode)
     tu, lu, _ = run(cfg, 0, prompt, 300, False)
-    te, le, _ = run(cfg, 0, prompt, 40, True, use_graph=False)
+    te, le, _ = run(cfg, 0, prompt, 40, mode, use_graph=False)
     np.testing.assert_array_equal(tf, tu)
     np.testing.assert_array_equal(lf, lu)
     np.testing.assert_array_equal(te, tu[:40])
