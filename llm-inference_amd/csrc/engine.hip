@@ -103,6 +103,10 @@ struct Engine {
     char* pf = nullptr;
     int pf_rows = 0;
     float *pf_x = nullptr, *pf_qkv = nullptr, *pf_o = nullptr, *pf_act = nullptr;
+    _Float16 *pf_ah = nullptr, *pf_al = nullptr;  // fp16 activation planes (gemm2 path)
+    float* pf_slab = nullptr;      // split-K partial slabs of the o_proj / down GEMMs [kPfSplit][R][H]
+    int pf_pending = 0;            // slices in pf_slab not yet added into pf_x
+    static constexpr int kPfSplit = 2;
     int host_next_pos = 0, prompt_len = 0;
     unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
     uint64_t seed = 0;
@@ -582,13 +586,78 @@ struct Engine {
         auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, A); return o; };
         const size_t ox = take(R * c.hidden * 4), oq = take(R * (ql + 2 * kvrows) * 4), oo = take(R * ql * 4),
                      oa = take(R * il * 4);
+        const size_t wide = std::max<size_t>(std::max<size_t>(c.hidden, ql), il);
+        const size_t oh = take(R * wide * 2), ol = take(R * wide * 2), os = take(kPfSplit * R * c.hidden * 4);
         LLMI_HIP(hipMalloc(&pf, off));
+        pf_slab = (float*)(pf + os);
+        pf_ah = (_Float16*)(pf + oh);
+        pf_al = (_Float16*)(pf + ol);
         pf_x = (float*)(pf + ox);
         pf_qkv = (float*)(pf + oq);
         pf_o = (float*)(pf + oo);
         pf_act = (float*)(pf + oa);
         return LLMI_OK;
     }
+
+    // One prefill layer on the LDS-DMA GEMM (gemm2.hip): RMSNorm + split into fp16
+    // planes, q/k/v GEMM, rope + KV write + causal attention, split, o_proj (+residual),
+    // RMSNorm + split, gate_up GEMM writing silu(g) * u as planes, down (+residual).
+    int prefill_layer_gemm2(int l, int m, int p0, int split) {
+        const Layer& L = layers[l];
+        const int H = c.hidden;
+        const size_t eb = dtype_size(c.kv_dtype);
+        _Float16* lo = split == 2 ? pf_al : nullptr;
+        Gemm2Args g;
+        g.a[0] = pf_ah; g.a[1] = lo; g.planes = split; g.m = m;
+        // (previous down slices into x) + rmsnorm + qkv
+        LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.attn_norm, edt, c.rms_eps, pf_ah, lo, H, stream,
+                                   pf_pending ? pf_slab : nullptr, pf_pending));
+        pf_pending = 0;
+        g.lda = H; g.w = L.qkv; g.n = ql + 2 * kvrows; g.k = H;
+        g.epi = EPI_STORE; g.y = pf_qkv; g.ldy = g.n;
+        LLMI_TRY(gemm2_launch(g, stream));
+        // rope + kv write + causal attention
+        PrefillAttnArgs pa;
+        pa.qkv = pf_qkv;
+        pa.k_cache = (char*)kcache + (size_t)l * kv_layer_elems * eb;
+        pa.v_cache = (char*)vcache + (size_t)l * kv_layer_elems * eb;
+        pa.cache_dtype = c.kv_dtype; pa.max_seq = c.max_seq; pa.m = m; pa.p0 = p0;
+        pa.heads = hl; pa.kv_heads = kvl; pa.head_dim = c.head_dim; pa.rope_tab = rope_tab; pa.out = pf_o;
+        LLMI_TRY(prefill_attn_launch(pa, stream));
+        // o_proj + residual (head-major W_o)
+        LLMI_TRY(rows_split_launch(pf_o, ql, m, ql, nullptr, edt, 0.f, pf_ah, lo, ql, stream));
+        // split-K into slabs (128 tiles alone would leave half the CUs idle); the next
+        // rows_split adds the slices into x in slice order (deterministic)
+        const int so = (ql % (kPfSplit * c.head_dim)) == 0 ? kPfSplit : 1;
+        g.lda = ql; g.w = L.o; g.w_kblock = c.head_dim; g.n = H; g.k = ql;
+        g.epi = EPI_SLAB; g.ksplit = so; g.slab = pf_slab; g.y = pf_x; g.ldy = H;
+        LLMI_TRY(gemm2_launch(g, stream));
+        g.w_kblock = 0;
+        // (o slices into x) + rmsnorm + gate_up + silu * up -> planes of the down GEMM's input
+        LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.ffn_norm, edt, c.rms_eps, pf_ah, lo, H, stream, pf_slab, so));
+        g.lda = H; g.w = L.gu; g.n = 2 * il; g.k = H;
+        g.epi = EPI_SILU_MUL; g.pair_off = il; g.y = nullptr; g.y_hi = pf_act_h(); g.y_lo = split == 2 ? pf_act_l() : nullptr;
+        g.ldy = il;
+        LLMI_TRY(gemm2_launch(g, stream));
+        // down + residual
+        g.a[0] = pf_act_h(); g.a[1] = split == 2 ? pf_act_l() : nullptr;
+        const int sd = (il % (kPfSplit * 64)) == 0 ? kPfSplit : 1;
+        g.lda = il; g.w = L.down; g.n = H; g.k = il;
+        g.epi = EPI_SLAB; g.ksplit = sd; g.pair_off = 0; g.y = pf_x; g.y_hi = g.y_lo = nullptr; g.ldy = H;
+        LLMI_TRY(gemm2_launch(g, stream));
+        pf_pending = sd;  // added by the next layer's rows_split (or prefill_flush)
+        return LLMI_OK;
+    }
+    int prefill_flush(int m) {  // pending down slices into x (after the last layer)
+        if (!pf_pending) return LLMI_OK;
+        LLMI_TRY(rows_split_launch(pf_x, c.hidden, m, c.hidden, nullptr, edt, 0.f, nullptr, nullptr, c.hidden, stream,
+                                   pf_slab, pf_pending));
+        pf_pending = 0;
+        return LLMI_OK;
+    }
+    // the SiLU output planes reuse pf_act's bytes (fp32 [R, il] = two fp16 planes)
+    _Float16* pf_act_h() { return reinterpret_cast<_Float16*>(pf_act); }
+    _Float16* pf_act_l() { return reinterpret_cast<_Float16*>(pf_act) + (size_t)pf_rows * il; }
 
     int prefill(int n, int split) {
         LLMI_REQUIRE(!grouped && c.tp_world == 1, "prefill: tensor-parallel prefill is not supported");
@@ -599,6 +668,10 @@ struct Engine {
             !gemm_supported(wdt, 2 * il, c.hidden, EPI_SILU_MUL) || !gemm_supported(wdt, c.hidden, il, EPI_ADD))
             return decode(n, 1);  // fp32 weights / odd shapes: the decode kernels, one row at a time
         LLMI_TRY(alloc_prefill());
+        const bool legacy = std::getenv("LLMI_PREFILL_LEGACY") != nullptr;  // A/B: register-staged GEMM
+        const bool use_gemm2 = !legacy && wdt == LLMI_F16 && gemm2_supported(ql + 2 * kvrows, c.hidden, EPI_STORE) &&
+                               gemm2_supported(c.hidden, ql, EPI_ADD) && gemm2_supported(2 * il, c.hidden, EPI_SILU_MUL) &&
+                               gemm2_supported(c.hidden, il, EPI_ADD) && c.head_dim % 64 == 0;
         const int H = c.hidden, p_begin = host_next_pos;
         const size_t eb = dtype_size(c.kv_dtype);
         for (int p0 = p_begin; p0 < p_begin + n; p0 += pf_rows) {
@@ -606,6 +679,10 @@ struct Engine {
             LLMI_TRY(embedding_launch(prompt + p0, m, embed, edt, c.vocab, H, pf_x, stream));
             for (int l = 0; l < c.layers; ++l) {
                 const Layer& L = layers[l];
+                if (use_gemm2) {
+                    LLMI_TRY(prefill_layer_gemm2(l, m, p0, split));
+                    continue;
+                }
                 GemmArgs g;
                 g.split = split;
                 g.w_dtype = wdt;
@@ -640,6 +717,7 @@ struct Engine {
                 g.epi = EPI_ADD; g.pair_off = 0; g.y = pf_x; g.ldy = H;
                 LLMI_TRY(gemm_launch(g, stream));
             }
+            LLMI_TRY(prefill_flush(m));
             if (p0 + m == p_begin + n) {  // last row -> final norm + lm_head + argmax keys
                 LLMI_HIP(hipMemcpyAsync(x, pf_x + (size_t)(m - 1) * H, (size_t)H * 4, hipMemcpyDeviceToDevice, stream));
                 LLMI_TRY(gemv_launch(lm_args(true), stream));

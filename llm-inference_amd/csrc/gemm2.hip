@@ -1,0 +1,334 @@
+// Prefill linear layers, fp16 weights, on the matrix cores with LDS-DMA staging
+// (SURVEY.md §8 a15, config 3):
+//   Y[m, n] (op)= sum_p sum_k A_p[m, k] * W[n, k]      (nn.Linear, W row-major [out, in])
+// the M = prompt-rows case of launchLinearGemm (linear.cu:38-99 -> cublasGemmEx with
+// trans_b, called from context_attention.cpp:99,166 and ffn.cpp:72,89).
+//
+// Numerics. W is fp16, so it enters the f16 MFMA exactly. The fp32 activations
+// arrive as P fp16 planes written by the producer (rows_split_kernel below, or the
+// gate_up epilogue): P = 2 is hi = fp16(a), lo = fp16(a - hi), both multiplied
+// against the same W fragment and accumulated in fp32 -- fp32-faithful
+// (|a - hi - lo| <= 2^-22 |a|); P = 1 is plain fp16 activations (the throughput
+// mode; 2.3e-3 logits rel-L2 over 32 layers vs the fp32 reference).
+// The RMSNorm of x (modeling_llama.py:112-117: x * rsqrt(mean(x^2) + eps), then
+// * gamma) is applied by rows_split_kernel while it writes the planes.
+//
+// Structure for gfx950 (cdna_hip_programming.md §5 "Async global->LDS copy" and
+// the 128^2 "step-3" structure): a BM x 128 output tile per 256-thread workgroup
+// (4 waves, 2 x 2, each (BM/2) x 64 = (BM/32) x 4 v_mfma_f32_16x16x32_f16 tiles),
+// BK = 64, operands staged global -> LDS by global_load_lds_dwordx4 (no VGPRs,
+// no ds_write pass) into two LDS stages: stage k+1 is in flight while stage k is
+// multiplied. The LDS image is lane-linear (the DMA writes wave base + 16 * lane)
+// with the st_16x32 XOR swizzle (byte bit 5 ^= bit 9) applied on the global
+// SOURCE address, so the fragment ds_read_b128s spread over the banks. Workgroup
+// ids are remapped (bijectively) so consecutive tiles share an XCD.
+// Roofline: MFMA (fp16 dense 2.5 PFLOP/s); FLOPs per launch 2 * M * N * K
+// (P = 2 issues 2x that on the matrix cores).
+#include <algorithm>
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace llmi {
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kBN = 128;
+constexpr int kBK = 64;
+constexpr int kRowB = kBK * 2;  // 128-B LDS rows
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) const void* glb_ptr_t;
+
+__device__ __forceinline__ int swz(int b) { return b ^ (((b >> 9) & 1) << 5); }
+__device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
+
+// SILU pairing (as gemm.hip): tile row tr of the B tile holds gate column
+// g0 + 32 (tr >> 6) + (tr & 31) for (tr & 32) == 0, its up row (+ pair_off) otherwise,
+// so a lane's n-fragments 0, 1 hold gate columns and 2, 3 the matching up columns.
+__device__ __forceinline__ int b_src_row(int epi, int n0, int tr, int pair_off) {
+    if (epi != EPI_SILU_MUL) return n0 + tr;
+    const int gc = n0 + 32 * (tr >> 6) + (tr & 31);
+    return (tr & 32) ? pair_off + gc : gc;
+}
+
+template <int BM, int P, int EPI>
+__global__ __launch_bounds__(kThreads) void gemm2_kernel(Gemm2Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int A_BYTES = BM * kRowB;          // one plane of one stage
+    constexpr int B_BYTES = kBN * kRowB;
+    constexpr int STAGE = P * A_BYTES + B_BYTES;
+    constexpr int A_GL = A_BYTES / (kThreads * 16);  // DMA instructions per thread per plane
+    constexpr int B_GL = B_BYTES / (kThreads * 16);
+    constexpr int MI = BM / 32;                  // 16-row fragments per wave
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w >> 1, wc = w & 1;
+
+    // bijective XCD remap: blocks sharing bid % 8 get consecutive tile ids
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int S = (EPI == EPI_SLAB) ? a.ksplit : 1;  // split-K: slices of one tile are consecutive ids
+    const int tile = id / S, slice = id - tile * S;
+    const int rt = tile / a.n_tiles, ct = tile - rt * a.n_tiles;
+    const int m0 = rt * BM;
+    const int n0 = (EPI == EPI_SILU_MUL) ? ct * (kBN / 2) : ct * kBN;
+    const int K = a.k / S;                            // this slice's K extent, from k_begin
+    const int k_begin = slice * K;
+    const size_t ldb = a.w_kblock ? (size_t)a.w_kblock : (size_t)a.k;  // W row stride (full K)
+
+    // per-thread DMA sources: instruction j of this thread fills LDS bytes
+    // j * 4096 + 16 t (lane-linear); that slot holds logical byte swz(.) of the tile
+    const char* a_src[P][A_GL];
+    const char* b_src[B_GL];
+#pragma unroll
+    for (int j = 0; j < A_GL; ++j) {
+        const int b = swz(j * kThreads * 16 + t * 16);
+        const int row = min(m0 + (b >> 7), a.m - 1);
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            a_src[p][j] = reinterpret_cast<const char*>(a.a[p]) + ((size_t)row * a.lda) * 2 + (b & 127);
+    }
+#pragma unroll
+    for (int j = 0; j < B_GL; ++j) {
+        const int b = swz(j * kThreads * 16 + t * 16);
+        const int src = b_src_row(EPI, n0, b >> 7, a.pair_off);
+        b_src[j] = reinterpret_cast<const char*>(a.w) + (size_t)src * ldb * 2 + (b & 127);
+    }
+    auto issue = [&](int stage, int kl) {
+        const int k0 = k_begin + kl;
+        char* base = lds + stage * STAGE + w * 1024;  // wave-uniform DMA base
+        const size_t koff =
+            (a.w_kblock ? (size_t)(k0 / a.w_kblock) * a.n * a.w_kblock + k0 % a.w_kblock : (size_t)k0) * 2;
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int j = 0; j < A_GL; ++j)
+                __builtin_amdgcn_global_load_lds((glb_ptr_t)(a_src[p][j] + (size_t)k0 * 2),
+                                                 (lds_ptr_t)(base + p * A_BYTES + j * kThreads * 16), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < B_GL; ++j)
+            __builtin_amdgcn_global_load_lds((glb_ptr_t)(b_src[j] + koff),
+                                             (lds_ptr_t)(base + P * A_BYTES + j * kThreads * 16), 16, 0, 0);
+    };
+
+    f4 acc[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int KT = K / kBK;
+    issue(0, 0);
+    for (int kt = 0; kt < KT; ++kt) {
+        // stage kt landed (every wave's DMAs drained, then the barrier publishes them);
+        // every wave also finished reading stage kt - 1, which the next issue overwrites
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + 1 < KT) issue((kt + 1) & 1, (kt + 1) * kBK);
+        const char* As = lds + (kt & 1) * STAGE;
+        const char* Bs = As + P * A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < kBK / 32; ++kk) {
+            const int kb = kk * 64 + fq * 16;
+            h8 bf[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                bf[j] = *reinterpret_cast<const h8*>(Bs + swz((wc * 64 + j * 16 + fr) * kRowB + kb));
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                const int ab = swz((wr * (BM / 2) + i * 16 + fr) * kRowB + kb);
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const h8 af = *reinterpret_cast<const h8*>(As + p * A_BYTES + ab);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    // epilogue: C fragment (i, j) register r is row 16 i + 4 (lane >> 4) + r, column 16 j + (lane & 15)
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wr * (BM / 2) + 16 * i + 4 * fq + r;
+            if (m >= a.m) continue;
+            if (EPI == EPI_SILU_MUL) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int gc = n0 + 32 * wc + 16 * j + fr;
+                    const float v = silu_f(acc[i][j][r]) * acc[i][j + 2][r];
+                    const size_t o = (size_t)m * a.ldy + gc;
+                    if (a.y_hi) {  // the down GEMM's input planes, written directly
+                        const _Float16 hi = (_Float16)v;
+                        a.y_hi[o] = hi;
+                        if (a.y_lo) a.y_lo[o] = (_Float16)(v - (float)hi);
+                    } else {
+                        a.y[o] = v;
+                    }
+                }
+            } else {
+                float* yrow = (EPI == EPI_SLAB ? a.slab + (size_t)slice * a.m * a.ldy : a.y) + (size_t)m * a.ldy;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int n = n0 + wc * 64 + 16 * j + fr;
+                    if (EPI == EPI_ADD)
+                        yrow[n] += acc[i][j][r];
+                    else
+                        yrow[n] = acc[i][j][r];
+                }
+            }
+        }
+    }
+}
+
+// RMSNorm (optional) + split of fp32 rows into fp16 planes: one workgroup per row.
+// v = x * rsqrt(mean(x^2) + eps) * gamma (the reference's order, modeling_llama.py:
+// 112-117); hi = fp16(v), lo = fp16(v - hi).
+__global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx, int k, const void* gamma,
+                                                             int g_dtype, float eps, _Float16* hi, _Float16* lo,
+                                                             int ldh, const float* slab, int ksplit, int m) {
+    __shared__ float red[16];
+    float* xr = x + (size_t)blockIdx.x * ldx;
+    const int k4 = k / 4;
+    if (slab) {  // split-K combine: x += slice 0 + slice 1 + ... (fixed order), written back
+        for (int j = threadIdx.x; j < k4; j += kThreads) {
+            float4 v = reinterpret_cast<const float4*>(xr)[j];
+            for (int s = 0; s < ksplit; ++s) {
+                const float4 p = reinterpret_cast<const float4*>(slab + ((size_t)s * m + blockIdx.x) * ldx)[j];
+                v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+            }
+            reinterpret_cast<float4*>(xr)[j] = v;
+        }
+        if (!hi) return;
+        __syncthreads();
+    }
+    float rstd = 1.f;
+    if (gamma) {
+        float ss = 0.f;
+        for (int j = threadIdx.x; j < k4; j += kThreads) {
+            const float4 v = reinterpret_cast<const float4*>(xr)[j];
+            ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+        ss = block_sum(ss, red);
+        rstd = 1.0f / sqrtf(ss / (float)k + eps);
+    }
+    if (!hi) return;
+    _Float16* hr = hi + (size_t)blockIdx.x * ldh;
+    _Float16* lr = lo ? lo + (size_t)blockIdx.x * ldh : nullptr;
+    for (int j = threadIdx.x; j < k4; j += kThreads) {
+        const float4 x4 = reinterpret_cast<const float4*>(xr)[j];
+        float v[4] = {x4.x, x4.y, x4.z, x4.w};
+        if (gamma) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float g = g_dtype == LLMI_F16 ? __half2float(static_cast<const __half*>(gamma)[4 * j + e])
+                                                    : static_cast<const float*>(gamma)[4 * j + e];
+                v[e] = (v[e] * rstd) * g;
+            }
+        }
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            h[e] = (_Float16)v[e];
+            l[e] = (_Float16)(v[e] - (float)h[e]);
+        }
+        reinterpret_cast<h4*>(hr)[j] = h;
+        if (lr) reinterpret_cast<h4*>(lr)[j] = l;
+    }
+}
+
+template <int BM, int P, int EPI>
+int launch3(const Gemm2Args& a, int grid, hipStream_t s) {
+    constexpr size_t lds = 2 * (size_t)(P * BM * kRowB + kBN * kRowB);
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm2_kernel<BM, P, EPI>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+    }();
+    LLMI_REQUIRE(attr, "gemm2: cannot raise the dynamic LDS limit");
+    hipLaunchKernelGGL((gemm2_kernel<BM, P, EPI>), dim3(grid), dim3(kThreads), lds, s, a);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+template <int BM, int P>
+int launch2(const Gemm2Args& a, int grid, hipStream_t s) {
+    switch (a.epi) {
+        case EPI_STORE: return launch3<BM, P, EPI_STORE>(a, grid, s);
+        case EPI_ADD: return launch3<BM, P, EPI_ADD>(a, grid, s);
+        case EPI_SILU_MUL: return launch3<BM, P, EPI_SILU_MUL>(a, grid, s);
+        case EPI_SLAB: return launch3<BM, P, EPI_SLAB>(a, grid, s);
+    }
+    LLMI_REQUIRE(false, "gemm2: epilogue must be store, add, silu_mul or slab");
+}
+
+}  // namespace
+
+bool gemm2_supported(int n, int k, int epi) {
+    const int ncols = (epi == EPI_SILU_MUL) ? n / 2 : n;
+    const int tile = (epi == EPI_SILU_MUL) ? kBN / 2 : kBN;
+    return n > 0 && k > 0 && ncols % tile == 0 && k % kBK == 0;
+}
+
+int gemm2_bm(const Gemm2Args& a) {
+    if (a.epi == EPI_SLAB) return 128;  // split-K supplies the workgroups
+    static const int forced = [] {
+        const char* e = std::getenv("LLMI_GEMM2_BM");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (forced == 64 || forced == 128) return forced;
+    const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
+    const int nt = ncols / ((a.epi == EPI_SILU_MUL) ? kBN / 2 : kBN);
+    // 128-row tiles unless that leaves CUs idle
+    return ((a.m + 127) / 128) * nt >= 256 ? 128 : 64;
+}
+
+int gemm2_launch(Gemm2Args a, hipStream_t s) {
+    LLMI_REQUIRE(a.a[0] && a.w && a.m > 0, "gemm2: null operand or empty M");
+    LLMI_REQUIRE(a.planes == 1 || (a.planes == 2 && a.a[1]), "gemm2: planes must be 1 or 2 (with a[1])");
+    LLMI_REQUIRE(gemm2_supported(a.n, a.k, a.epi), "gemm2: N a multiple of 128 (gate_up: 2 x 64), K of 64");
+    LLMI_REQUIRE(a.epi == EPI_SILU_MUL ? (a.y || a.y_hi) : a.y != nullptr, "gemm2: null output");
+    LLMI_REQUIRE(a.lda % 8 == 0 && (reinterpret_cast<uintptr_t>(a.a[0]) & 15) == 0 &&
+                     (a.planes == 1 || (reinterpret_cast<uintptr_t>(a.a[1]) & 15) == 0),
+                 "gemm2: A planes must be 16-B aligned with lda % 8 == 0");
+    LLMI_REQUIRE((reinterpret_cast<uintptr_t>(a.w) & 15) == 0, "gemm2: W must be 16-B aligned");
+    LLMI_REQUIRE(a.w_kblock == 0 || (a.w_kblock % kBK == 0 && a.k % a.w_kblock == 0 && a.epi != EPI_SILU_MUL),
+                 "gemm2: w_kblock must be a multiple of 64 dividing K (not with the gate_up pairing)");
+    LLMI_REQUIRE(a.epi != EPI_SILU_MUL || a.pair_off == a.n / 2, "gemm2: gate_up pair offset must be N / 2");
+    const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
+    a.n_tiles = ncols / ((a.epi == EPI_SILU_MUL) ? kBN / 2 : kBN);
+    if (a.epi == EPI_SLAB) {
+        LLMI_REQUIRE(a.slab && a.ksplit >= 1 && a.k % (a.ksplit * kBK) == 0 &&
+                         (a.w_kblock == 0 || (a.k / a.ksplit) % a.w_kblock == 0),
+                     "gemm2: split-K needs a slab and K / ksplit a multiple of 64 (and of w_kblock)");
+    } else {
+        a.ksplit = 1;
+    }
+    const int bm = gemm2_bm(a);
+    const int grid = ((a.m + bm - 1) / bm) * a.n_tiles * a.ksplit;
+    if (bm == 128) return a.planes == 2 ? launch2<128, 2>(a, grid, s) : launch2<128, 1>(a, grid, s);
+    return a.planes == 2 ? launch2<64, 2>(a, grid, s) : launch2<64, 1>(a, grid, s);
+}
+
+int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,
+                      _Float16* lo, int ldh, hipStream_t s, const float* slab, int ksplit) {
+    LLMI_REQUIRE(x && (hi || slab) && m > 0 && k > 0 && k % 4 == 0 && ldx % 4 == 0 && ldh % 4 == 0,
+                 "rows_split: bad arguments");
+    LLMI_REQUIRE(!slab || (ksplit >= 1 && ldx == k), "rows_split: slab rows must be dense (ldx == k)");
+    hipLaunchKernelGGL(rows_split_kernel, dim3(m), dim3(kThreads), 0, s, x, ldx, k, gamma, g_dtype, eps, hi, lo, ldh,
+                       slab, ksplit, m);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace llmi

@@ -14,6 +14,7 @@ enum GemvEpi : int {
     EPI_SILU_MUL = 2,  // rows (g, g + pair_off): y[g] = silu(acc0) * acc1
     EPI_ARGMAX = 3,    // y[r] = acc; per-block argmax key -> partials[blockIdx]
     EPI_ATOMIC = 4,    // yacc[r] += fixed(acc) (int64 2^-32 units; exact, order-independent), split-K
+    EPI_SLAB = 5,      // gemm2 split-K: partial [slice][m][ldy] stored; the next rows_split adds the slices in order
 };
 
 struct GemvArgs {
@@ -76,6 +77,32 @@ struct GemmArgs {
 bool gemm_supported(int w_dtype, int n, int k, int epi);
 int gemm_bm(const GemmArgs& a);
 int gemm_launch(GemmArgs a, hipStream_t s);
+
+// LDS-DMA MFMA GEMM for fp16 weights (gemm2.hip): A arrives as `planes` fp16
+// planes (hi[, lo]) written by rows_split_launch or the gate_up epilogue.
+struct Gemm2Args {
+    const _Float16* a[2] = {nullptr, nullptr};  // [m, lda] planes
+    int planes = 2;
+    int lda = 0;
+    const void* w = nullptr;       // [n, k] fp16 (or head-major blocks, w_kblock)
+    int w_kblock = 0;
+    int m = 0, n = 0, k = 0;
+    int epi = EPI_STORE;           // EPI_STORE, EPI_ADD, EPI_SILU_MUL
+    int pair_off = 0;
+    float* y = nullptr;            // [m, ldy] fp32
+    _Float16* y_hi = nullptr;      // EPI_SILU_MUL: write the result as fp16 planes instead
+    _Float16* y_lo = nullptr;
+    int ldy = 0;
+    int ksplit = 1;                // EPI_SLAB: K slices (K / ksplit a multiple of 64, and of w_kblock)
+    float* slab = nullptr;         // EPI_SLAB: [ksplit][m][ldy] partial sums
+    int n_tiles = 0;               // set by gemm2_launch
+};
+bool gemm2_supported(int n, int k, int epi);
+int gemm2_launch(Gemm2Args a, hipStream_t s);
+// rows of x (+= the ksplit slices of slab, in slice order, written back to x),
+// then optional RMSNorm, then fp16 planes hi[, lo] (hi null: the combine alone)
+int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,
+                      _Float16* lo, int ldh, hipStream_t s, const float* slab = nullptr, int ksplit = 0);
 
 // ------------------------------------------------- prefill attention
 // rope + KV-cache write of M rows, then causal attention over cache slots
