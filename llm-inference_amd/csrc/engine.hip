@@ -98,6 +98,7 @@ struct Engine {
     int fuse_mode = 0;
     bool fused = false;            // fuse_mode == 1
     int down_ksplit = 1;           // K-slices of the down projection (int64 atomic epilogue)
+    int grid_qkv = 0, grid_gu = 0, grid_down = 0;  // GEMV grid overrides (0: gemv_grid's choice)
     unsigned* layer_cnt = nullptr; // [layers][layer_cnt_words()] counters, zeroed by step_start
     // prefill scratch (allocated on first use): rows of one prefill chunk
     char* pf = nullptr;
@@ -278,6 +279,9 @@ struct Engine {
             fused = fuse_mode == 1;
             const char* ks = std::getenv("LLMI_DOWN_KSPLIT");
             down_ksplit = ks ? std::max(1, std::atoi(ks)) : (fused ? 4 : 1);
+            grid_qkv = env_int("LLMI_GRID_QKV");  // tuning overrides
+            grid_gu = env_int("LLMI_GRID_GU");
+            grid_down = env_int("LLMI_GRID_DOWN");
         }
         // cos/sin cache with HF's fp32 arithmetic (LlamaRotaryEmbedding._set_cos_sin_cache):
         // inv_freq = 1 / fp32(base ** (2i/d)) (torch's fp32 pow is correctly rounded),
@@ -368,6 +372,10 @@ struct Engine {
         return a;
     }
 
+    static int env_int(const char* name) {
+        const char* e = std::getenv(name);
+        return e ? std::atoi(e) : 0;
+    }
     GemvArgs qkv_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
@@ -376,6 +384,7 @@ struct Engine {
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
+        a.grid = grid_qkv;
         if (fuse_mode == 3) {  // the fused attention + o_proj adds into xacc from its first workgroup on:
             a.seed_src = res[l % 2]; a.seed_dst = xacc; a.seed_n = c.hidden;  // seed it here
             a.seed_keep = c.tp_rank == 0 ? 1 : 0;                               // (rank 0 carries the residual)
@@ -431,6 +440,7 @@ struct Engine {
         a.seed_keep = c.tp_rank == 0 ? 1 : 0;
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
+        a.grid = grid_gu;
         return a;
     }
     GemvArgs down_args(int l) const {
@@ -441,6 +451,7 @@ struct Engine {
         a.n_rows = c.hidden; a.k = il; a.x = act;
         a.epi = EPI_ATOMIC; a.yacc = res[(l + 1) % 2];
         a.ksplit = (il % (down_ksplit * (16 / (int)wsz))) == 0 ? down_ksplit : 1;
+        a.grid = grid_down ? grid_down * a.ksplit : 0;
         return a;
     }
 
@@ -623,9 +634,12 @@ struct Engine {
         pa.v_cache = (char*)vcache + (size_t)l * kv_layer_elems * eb;
         pa.cache_dtype = c.kv_dtype; pa.max_seq = c.max_seq; pa.m = m; pa.p0 = p0;
         pa.heads = hl; pa.kv_heads = kvl; pa.head_dim = c.head_dim; pa.rope_tab = rope_tab; pa.out = pf_o;
+        if (c.kv_dtype == LLMI_F16) {  // MFMA attention writes the o_proj input planes itself
+            pa.mfma_planes = split; pa.out_hi = pf_ah; pa.out_lo = lo;
+        }
         LLMI_TRY(prefill_attn_launch(pa, stream));
         // o_proj + residual (head-major W_o)
-        LLMI_TRY(rows_split_launch(pf_o, ql, m, ql, nullptr, edt, 0.f, pf_ah, lo, ql, stream));
+        if (c.kv_dtype != LLMI_F16) LLMI_TRY(rows_split_launch(pf_o, ql, m, ql, nullptr, edt, 0.f, pf_ah, lo, ql, stream));
         // split-K into slabs (128 tiles alone would leave half the CUs idle); the next
         // rows_split adds the slices into x in slice order (deterministic)
         const int so = (ql % (kPfSplit * c.head_dim)) == 0 ? kPfSplit : 1;

@@ -117,6 +117,11 @@ struct PrefillAttnArgs {
     int heads = 0, kv_heads = 0, head_dim = 128;
     const float* rope_tab = nullptr;  // [max_seq][D/2] (cos, sin)
     float* out = nullptr;          // [m, heads * D]
+    // fp16 cache only: 1 or 2 = the MFMA kernel with that many fp16 planes of q and
+    // p (2: fp32-faithful); out_hi (, out_lo) given: write the output as fp16 planes
+    int mfma_planes = 0;
+    _Float16* out_hi = nullptr;
+    _Float16* out_lo = nullptr;
 };
 int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s);
 // after a prefill of prompt rows [p0, p0 + n): record them as tokens and

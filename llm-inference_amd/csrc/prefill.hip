@@ -183,6 +183,208 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_kernel(const float* qkv
     }
 }
 
+// ---- MFMA form for the fp16 cache (engine prefill). Workgroup = (64 query rows,
+// head): wave w owns rows 16 w .. 16 w + 15. Per 64-key block of the causal range:
+//   S = Q K^T     v_mfma_f32_16x16x32_f16, Q fragments in registers (q * 1/sqrt(d)
+//                 split into P fp16 planes), K staged in LDS [key][dim] with the
+//                 16-B chunk index XOR (key & 15): a B fragment's 16 rows hit 16
+//                 distinct bank groups;
+//   online softmax on the accumulator layout (rows 4 (lane >> 4) + r), fp32 expf;
+//   O += P V      P through a per-wave LDS image (C layout -> A layout, P planes),
+//                 V staged transposed [dim][key] (chunk XOR (dim & 7)).
+// The next block's K/V rows are loaded into registers before this block's MFMAs
+// (register double buffer). P = 2 (hi + lo planes of q and of p against the exact
+// fp16 K, V) is fp32-faithful; P = 1 is the fp16 throughput mode. Output: fp32 rows,
+// or the o_proj GEMM's fp16 input planes directly.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int QM = 64;  // query rows per workgroup
+constexpr int KB = 64;  // keys per block
+
+template <int P>
+__global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float* qkv, int ld, int m_rows, int p0,
+                                                                     int heads, int kv_heads, const __half* k_cache,
+                                                                     const __half* v_cache, int max_seq, float* out,
+                                                                     _Float16* out_hi, _Float16* out_lo, int ldo) {
+    __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 + D * KB * 2 + 4 * P * 16 * KB * 2];
+    char* Ks = smem;                 // [key][256 B], chunk ^= key & 15
+    char* Vt = smem + KB * D * 2;    // [dim][128 B], chunk ^= dim & 7
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    char* Pw = Vt + D * KB * 2 + w * P * 16 * KB * 2;  // this wave's [P][16][128 B], chunk ^= row & 7
+
+    const int qb = gridDim.x - 1 - blockIdx.x;  // longest (latest) query blocks first
+    const int h = blockIdx.y;
+    const int kvh = h / (heads / kv_heads);
+    const int q_first = qb * QM;
+    const float qscale = 1.0f / sqrtf((float)D);
+
+    // Q fragments: row q_first + 16 w + fr, dims 32 ks + 8 fq + [0, 8)
+    h8 qa[P][4];
+    {
+        const int qrow = min(q_first + 16 * w + fr, m_rows - 1);
+        const float* qp = qkv + (size_t)qrow * ld + (size_t)h * D;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const float4 a = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq);
+            const float4 b = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq + 4);
+            const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float x = v[e] * qscale;
+                const _Float16 hi = (_Float16)x;
+                qa[0][ks][e] = hi;
+                if (P == 2) qa[P - 1][ks][e] = (_Float16)(x - (float)hi);
+            }
+        }
+    }
+
+    const int kend = p0 + min(q_first + QM, m_rows);  // keys [0, kend)
+    const int nkb = (kend + KB - 1) / KB;
+    const __half* kc = k_cache + (size_t)kvh * max_seq * D;
+    const __half* vc = v_cache + (size_t)kvh * max_seq * D;
+    // staging: thread t moves 16 B (8 dims) of key rows t / 16 + 16 i, chunk t % 16
+    const int sr = t >> 4, sc = t & 15;
+    uint4 kreg[4], vreg[4];
+    auto gload = [&](int kb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int key = min(kb * KB + sr + 16 * i, kend - 1);
+            kreg[i] = *reinterpret_cast<const uint4*>(kc + (size_t)key * D + sc * 8);
+            vreg[i] = *reinterpret_cast<const uint4*>(vc + (size_t)key * D + sc * 8);
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = sr + 16 * i;
+            *reinterpret_cast<uint4*>(Ks + r * 256 + ((sc ^ (r & 15)) << 4)) = kreg[i];
+            const _Float16* hv = reinterpret_cast<const _Float16*>(&vreg[i]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int d = sc * 8 + e;
+                *reinterpret_cast<_Float16*>(Vt + d * 128 + (((r >> 3) ^ (d & 7)) << 4) + (r & 7) * 2) = hv[e];
+            }
+        }
+    };
+
+    float m_run[4], l_run[4];
+    f4 o[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m_run[r] = -INFINITY;
+        l_run[r] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f4{0.f, 0.f, 0.f, 0.f};
+    const int qpos0 = p0 + q_first + 16 * w + 4 * fq;  // position of accumulator row r: qpos0 + r
+
+    gload(0);
+    for (int kb = 0; kb < nkb; ++kb) {
+        __syncthreads();  // every wave finished reading the previous block
+        lstore();
+        __syncthreads();
+        if (kb + 1 < nkb) gload(kb + 1);
+
+        f4 s[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = 16 * j + fr;
+                const h8 bk = *reinterpret_cast<const h8*>(Ks + key * 256 + (((4 * ks + fq) ^ (key & 15)) << 4));
+#pragma unroll
+                for (int p = 0; p < P; ++p) s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[p][ks], bk, s[j], 0, 0, 0);
+            }
+        }
+        // causal mask (build_causal_mask.cu:29: key <= query position), online softmax
+        float mx[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            mx[r] = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = kb * KB + 16 * j + fr;
+                if (key > qpos0 + r || key >= kend) s[j][r] = -INFINITY;
+                mx[r] = fmaxf(mx[r], s[j][r]);
+            }
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
+        }
+        float alpha[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float m_new = fmaxf(m_run[r], mx[r]);  // finite: key 0 is visible to every row
+            alpha[r] = expf(m_run[r] - m_new);
+            m_run[r] = m_new;
+            float ps = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float pv = expf(s[j][r] - m_new);
+                s[j][r] = pv;
+                ps += pv;
+            }
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) ps += __shfl_xor(ps, off);
+            l_run[r] = l_run[r] * alpha[r] + ps;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
+        // P (C layout: row 4 fq + r, key 16 j + fr) -> this wave's LDS image
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * fq + r, key = 16 * j + fr;
+                const int off = row * 128 + (((key >> 3) ^ (row & 7)) << 4) + (key & 7) * 2;
+                const _Float16 hi = (_Float16)s[j][r];
+                *reinterpret_cast<_Float16*>(Pw + off) = hi;
+                if (P == 2) *reinterpret_cast<_Float16*>(Pw + 16 * KB * 2 + off) = (_Float16)(s[j][r] - (float)hi);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // O += P V: A = P rows fr, keys 32 kk + 8 fq; B = V^T rows (dims) 16 jt + fr
+#pragma unroll
+        for (int kk = 0; kk < KB / 32; ++kk) {
+            h8 pa[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+                pa[p] = *reinterpret_cast<const h8*>(Pw + p * 16 * KB * 2 + fr * 128 + (((4 * kk + fq) ^ (fr & 7)) << 4));
+#pragma unroll
+            for (int jt = 0; jt < 8; ++jt) {
+                const int d = 16 * jt + fr;
+                const h8 bv = *reinterpret_cast<const h8*>(Vt + d * 128 + (((4 * kk + fq) ^ (d & 7)) << 4));
+#pragma unroll
+                for (int p = 0; p < P; ++p) o[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[p], bv, o[jt], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // P image is rewritten next block
+    }
+
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = q_first + 16 * w + 4 * fq + r;
+        if (row >= m_rows) continue;
+        const float inv = 1.0f / l_run[r];
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) {
+            const size_t idx = (size_t)row * ldo + (size_t)h * D + 16 * jt + fr;
+            const float v = o[jt][r] * inv;
+            if (out_hi) {
+                const _Float16 hi = (_Float16)v;
+                out_hi[idx] = hi;
+                if (out_lo) out_lo[idx] = (_Float16)(v - (float)hi);
+            } else {
+                out[idx] = v;
+            }
+        }
+    }
+}
+
 __global__ void prefill_finish_kernel(DecodeState* st, const int32_t* prompt, int32_t* tokens, int p0, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) tokens[p0 + i] = prompt[p0 + i];
     if (threadIdx.x == 0) {
@@ -201,18 +403,34 @@ int prefill_finish_launch(DecodeState* st, const int32_t* prompt, int32_t* token
 }
 
 int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
-    LLMI_REQUIRE(a.qkv && a.k_cache && a.v_cache && a.out && a.rope_tab, "prefill attention: null argument");
+    LLMI_REQUIRE(a.qkv && a.k_cache && a.v_cache && a.rope_tab, "prefill attention: null argument");
     LLMI_REQUIRE(a.head_dim == D, "prefill attention: head_dim must be 128");
     LLMI_REQUIRE(a.m > 0 && a.p0 >= 0 && a.p0 + a.m <= a.max_seq, "prefill attention: rows past max_seq");
     LLMI_REQUIRE(a.heads > 0 && a.kv_heads > 0 && a.heads % a.kv_heads == 0, "prefill attention: bad head counts");
+    LLMI_REQUIRE(a.mfma_planes == 0 || ((a.mfma_planes == 1 || a.mfma_planes == 2) && a.cache_dtype == LLMI_F16 &&
+                                        (a.out || a.out_hi)),
+                 "prefill attention: the MFMA form needs the fp16 cache, 1 or 2 planes and an output");
+    LLMI_REQUIRE(a.mfma_planes != 0 || a.out, "prefill attention: null output");
     const int ld = (a.heads + 2 * a.kv_heads) * D;
     const dim3 ga((a.m + QB - 1) / QB, a.heads);
     if (a.cache_dtype == LLMI_F16) {
         hipLaunchKernelGGL(rope_kv_prefill_kernel<__half>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (__half*)a.k_cache, (__half*)a.v_cache, a.max_seq);
-        hipLaunchKernelGGL(attn_prefill_kernel<__half>, ga, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0, a.heads,
-                           a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq, a.out,
-                           a.heads * D);
+        if (a.mfma_planes) {
+            const dim3 gm((a.m + QM - 1) / QM, a.heads);
+            if (a.mfma_planes == 2)
+                hipLaunchKernelGGL(attn_prefill_mfma_kernel<2>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
+                                   a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
+                                   a.out, a.out_hi, a.out_lo, a.heads * D);
+            else
+                hipLaunchKernelGGL(attn_prefill_mfma_kernel<1>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
+                                   a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
+                                   a.out, a.out_hi, a.out_lo, a.heads * D);
+        } else {
+            hipLaunchKernelGGL(attn_prefill_kernel<__half>, ga, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0, a.heads,
+                               a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq, a.out,
+                               a.heads * D);
+        }
     } else if (a.cache_dtype == LLMI_F32) {
         hipLaunchKernelGGL(rope_kv_prefill_kernel<float>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (float*)a.k_cache, (float*)a.v_cache, a.max_seq);
