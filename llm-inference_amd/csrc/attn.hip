@@ -41,6 +41,68 @@ __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
     attn_body<KT, PlainIO>(a, blockIdx.x, blockIdx.y, gridDim.y, smem, NoSync{});
 }
 
+// attention + merge by the last-arriving split workgroup of each head (the
+// split-K "last block reduces" form, cdna_hip_programming.md §5 Projection GEMM
+// item 2, sc1 variant): partials are stored write-through and drained, one
+// agent-scope ticket per workgroup, the workgroup that draws nact - 1 reads every
+// partial of its head with sc1 loads, merges (same arithmetic as the o_proj merge)
+// and writes merge_out; it re-zeroes the head's ticket for the next launch.
+struct PartialSc1IO : PlainIO {
+    __device__ __forceinline__ static void st(float* p, float v) { Sc1IO::st(p, v); }
+};
+template <typename KT>
+__global__ __launch_bounds__(kThreads) void attn_decode_merge_kernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    WgStamp ts(a.stamps);
+    const int h = blockIdx.x, split = blockIdx.y, ns = gridDim.y, tid = threadIdx.x;
+    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
+    if (pos < 0 || pos >= a.max_seq) return;
+    const int nact = (pos + 1 + CH - 1) / CH;
+    if (split >= nact) return;
+    attn_body<KT, PartialSc1IO>(a, h, split, ns, smem, NoSync{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 partials
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem + kAttnLds / 4);
+    Ws ws = ws_carve(a.workspace, a.heads, ns);
+    unsigned* ticket = ws.counters + (size_t)h * kCntWordsPerHead + 2;
+    if (tid == 0)
+        *last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nact - 1;
+    __syncthreads();
+    if (!*last) return;
+    if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float* m_s = smem;
+    float* l_s = smem + ns;
+    float* o2 = smem + 2 * ns;  // [2][D]
+    float* linv = o2 + 2 * D;
+    const float* mlh = ws.ml + (size_t)h * ns * 2;
+    const float* oh = ws.o + (size_t)h * ns * D;
+    for (int sp = tid; sp < nact; sp += kThreads) {
+        m_s[sp] = Sc1IO::ld(mlh + 2 * sp);
+        l_s[sp] = Sc1IO::ld(mlh + 2 * sp + 1);
+    }
+    __syncthreads();
+    if (tid < kWave) {
+        float M = -INFINITY;
+        for (int sp = tid; sp < nact; sp += kWave) M = fmaxf(M, m_s[sp]);
+        M = wave_max(M);
+        float lsum = 0.f;
+        for (int sp = tid; sp < nact; sp += kWave) {
+            const float wgt = expf(m_s[sp] - M);
+            m_s[sp] = wgt;
+            lsum = fmaf(l_s[sp], wgt, lsum);
+        }
+        lsum = wave_sum(lsum);
+        if (tid == 0) *linv = 1.0f / lsum;
+    }
+    __syncthreads();
+    const int d = tid % D, half = tid / D;
+    float O = 0.f;
+    for (int sp = half; sp < nact; sp += 2) O = fmaf(Sc1IO::ld(oh + (size_t)sp * D + d), m_s[sp], O);
+    o2[half * D + d] = O;
+    __syncthreads();
+    if (tid < D) a.merge_out[(size_t)h * D + tid] = (o2[tid] + o2[D + tid]) * *linv;
+}
+
 // Log-sum-exp merge of the split-KV partials of each head (one workgroup per
 // head, 2 threads per head dim). Every load it needs -- the position, (m, l) of
 // every split and up to 2 * kMergeChunk o-partials per dim -- is issued in one
@@ -132,10 +194,13 @@ struct HeadSync {
     int* err;
     __device__ __forceinline__ void wait() const {
         if (!LLMI_FUSED_NOWAIT && threadIdx.x == 0) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-            while (__hip_atomic_load(const_cast<unsigned*>(cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                   target) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 200 ms: give up, flag it
+            // the clock (a scalar-memory round trip) only once the counter was seen short
+            unsigned long long t0 = 0;
+            for (unsigned n = 0;; ++n) {
+                if (__hip_atomic_load(const_cast<unsigned*>(cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target)
+                    break;
+                if (n == 0) t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+                if ((n & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 200 ms: give up
                     if (err) atomicOr(err, 4);
                     break;
                 }
@@ -252,6 +317,19 @@ int attn_decode_launch(const AttnArgs& a, hipStream_t s) {
     LLMI_REQUIRE(!a.direct_out || a.out, "attn: null output");
     LLMI_REQUIRE(!a.xacc || a.resid || a.resid_fixed, "attn: xacc seeding needs resid");
     const dim3 grid(a.heads, (a.max_seq + CH - 1) / CH);  // ns = gridDim.y
+    if (a.merge_out) {
+        LLMI_REQUIRE(!a.direct_out && !a.xacc && a.pos_dev, "attn: merge_out needs the engine form (device position, no xacc)");
+        LLMI_REQUIRE(2 * (size_t)grid.y + 2 * D + 4 <= kAttnLds / 4, "attn: max_seq too large for the in-kernel merge");
+        const size_t lds = kAttnLds + 16;
+        if (a.cache_dtype == LLMI_F16)
+            hipLaunchKernelGGL(attn_decode_merge_kernel<__half>, grid, dim3(kThreads), lds, s, a);
+        else if (a.cache_dtype == LLMI_F32)
+            hipLaunchKernelGGL(attn_decode_merge_kernel<float>, grid, dim3(kThreads), lds, s, a);
+        else
+            LLMI_REQUIRE(false, "attn: cache dtype must be f16 or f32");
+        LLMI_HIP(hipGetLastError());
+        return LLMI_OK;
+    }
     if (a.cache_dtype == LLMI_F16)
         hipLaunchKernelGGL(attn_decode_kernel<__half>, grid, dim3(kThreads), kAttnLds, s, a);
     else if (a.cache_dtype == LLMI_F32)

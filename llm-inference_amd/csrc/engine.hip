@@ -99,6 +99,7 @@ struct Engine {
     bool fused = false;            // fuse_mode == 1
     int down_ksplit = 1;           // K-slices of the down projection (int64 atomic epilogue)
     int grid_qkv = 0, grid_gu = 0, grid_down = 0;  // GEMV grid overrides (0: gemv_grid's choice)
+    int ring_grid_n = 0;           // ring layer grid (one workgroup per CU)
     unsigned* layer_cnt = nullptr; // [layers][layer_cnt_words()] counters, zeroed by step_start
     // prefill scratch (allocated on first use): rows of one prefill chunk
     char* pf = nullptr;
@@ -271,7 +272,14 @@ struct Engine {
             // LLMI_FUSED=2: dataflow attention + o_proj phases (measured even);
             // LLMI_FUSED=3: attention + merge/o_proj co-scheduled per head in one launch
             //               (attn.hip; measured 21.8 vs 19.8 us for the two launches at ctx 2048)
-            fuse_mode = !env ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : env[0] == '3' ? 3 : 0;
+            //               LLMI_FUSED=4: ring layer (ring.hip): attention merges in-kernel, then
+            //               o_proj + gate_up + down as one persistent launch with an LDS-DMA weight ring
+            fuse_mode = !env ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : env[0] == '3' ? 3 : env[0] == '4' ? 4 : 0;
+            if (fuse_mode == 4) {
+                ring_grid_n = ring_grid(device);
+                if (wdt != LLMI_F16 || c.tp_world != 1 || grouped || ring_check(ring_args(0), device) != LLMI_OK)
+                    fuse_mode = 0;
+            }
             if (wdt == LLMI_F32 && (fuse_mode == 1 || fuse_mode == 2)) fuse_mode = 0;
             if (fuse_mode == 1 && (c.tp_world != 1 || grouped)) fuse_mode = 2;
             if (fuse_mode == 3 && attn_oproj_fused_check(attn_args_fused(0), o_args(0), device) != LLMI_OK)
@@ -319,11 +327,9 @@ struct Engine {
             LLMI_TRY(fill(L.qkv, 0, lin, wdt, t(prng::Q), ql, H, r * ql, 0, H));
             LLMI_TRY(fill(L.qkv, ql, lin, wdt, t(prng::K), kvrows, H, r * kvrows, 0, H));
             LLMI_TRY(fill(L.qkv, ql + kvrows, lin, wdt, t(prng::V), kvrows, H, r * kvrows, 0, H));
-            // W_o head-major, [hl][H][head_dim]: the o_proj workgroup of (head, row chunk)
-            // streams one contiguous slab instead of 256-B row segments 8 KB apart
-            for (int hh = 0; hh < hl; ++hh)
-                LLMI_TRY(fill(L.o, (size_t)hh * H, lin, wdt, t(prng::O), H, c.head_dim, 0, r * ql + hh * c.head_dim,
-                              c.heads * c.head_dim));
+            // W_o row-major [H, ql] (a head-major layout measured no faster for the
+            // split-by-head o_proj, and the ring layer streams whole rows)
+            LLMI_TRY(fill(L.o, 0, lin, wdt, t(prng::O), H, ql, 0, r * ql, c.heads * c.head_dim));
             // fused [gate; up] rows (layer_weights.cc:40 order)
             LLMI_TRY(fill(L.gu, 0, lin, wdt, t(prng::GATE), il, H, r * il, 0, H));
             LLMI_TRY(fill(L.gu, il, lin, wdt, t(prng::UP), il, H, r * il, 0, H));
@@ -391,6 +397,24 @@ struct Engine {
         }
         return a;
     }
+    AttnArgs attn_args_ring(int l) const {
+        AttnArgs a = attn_args(l);
+        a.xacc = nullptr;
+        a.merge_out = attn_out;  // merged per head in-kernel; the ring layer's o_proj input
+        return a;
+    }
+    RingArgs ring_args(int l) const {
+        const Layer& L = layers[l];
+        RingArgs a;
+        a.w_o = L.o; a.w_gu = L.gu; a.w_d = L.down; a.gamma = L.ffn_norm; a.eps = c.rms_eps;
+        a.hidden = c.hidden; a.q_dim = ql; a.inter = il;
+        a.attn = attn_out; a.resid = res[l % 2]; a.resid_keep = 1;
+        a.xmid = xacc; a.act = act; a.resid_out = res[(l + 1) % 2]; a.x_out = x;
+        a.cnt = layer_cnt + (size_t)l * layer_cnt_words();
+        a.err = &st->error;
+        a.stamps = dbg_stamps;
+        return a;
+    }
     AttnArgs attn_args_fused(int l) const {
         AttnArgs a = attn_args(l);
         a.xacc = nullptr;  // seeded by the q/k/v GEMV instead
@@ -421,7 +445,7 @@ struct Engine {
         OprojArgs a;
         a.stamps = dbg_stamps;
         a.w = L.o; a.scales = L.o_s; a.w_dtype = wdt;
-        a.head_major = 1;
+        a.head_major = 0;
         a.n_rows = c.hidden; a.ldw = ql;
         a.heads = hl; a.head_dim = c.head_dim; a.max_seq = c.max_seq;
         a.pos_dev = &st->cur_pos;
@@ -461,7 +485,7 @@ struct Engine {
     // group (struct Group) can interleave its ranks between the reductions.
     int rec_start() {
         return step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, res[0], c.max_seq,
-                                 (fuse_mode == 1 || fuse_mode == 2) ? layer_cnt : nullptr, c.layers * layer_cnt_words(), stream);
+                                 (fuse_mode == 1 || fuse_mode == 2 || fuse_mode == 4) ? layer_cnt : nullptr, c.layers * layer_cnt_words(), stream);
     }
     LayerArgs layer_args(int l) const {
         LayerArgs L;
@@ -491,6 +515,7 @@ struct Engine {
     int rec_attn(int l) {
         LLMI_TRY(gemv_launch(qkv_args(l), stream));
         if (fuse_mode == 3) return attn_oproj_fused_launch(attn_args_fused(l), o_args(l), &st->error, stream);
+        if (fuse_mode == 4) return attn_decode_launch(attn_args_ring(l), stream);
         if (fuse_mode == 2) {
             const int rc = layer_launch_phases(layer_args(l), 1, 2, stream);
             if (rc != LLMI_EUNSUPPORTED) return rc;
@@ -500,6 +525,7 @@ struct Engine {
         return attn_oproj_launch(o_args(l), stream);
     }
     int rec_ffn(int l) {
+        if (fuse_mode == 4) return ring_layer_launch(ring_args(l), ring_grid_n, stream);
         LLMI_TRY(gemv_launch(gu_args(l), stream));
         return gemv_launch(down_args(l), stream);
     }
@@ -638,12 +664,12 @@ struct Engine {
             pa.mfma_planes = split; pa.out_hi = pf_ah; pa.out_lo = lo;
         }
         LLMI_TRY(prefill_attn_launch(pa, stream));
-        // o_proj + residual (head-major W_o)
+        // o_proj + residual
         if (c.kv_dtype != LLMI_F16) LLMI_TRY(rows_split_launch(pf_o, ql, m, ql, nullptr, edt, 0.f, pf_ah, lo, ql, stream));
         // split-K into slabs (128 tiles alone would leave half the CUs idle); the next
         // rows_split adds the slices into x in slice order (deterministic)
-        const int so = (ql % (kPfSplit * c.head_dim)) == 0 ? kPfSplit : 1;
-        g.lda = ql; g.w = L.o; g.w_kblock = c.head_dim; g.n = H; g.k = ql;
+        const int so = (ql % (kPfSplit * 64)) == 0 ? kPfSplit : 1;
+        g.lda = ql; g.w = L.o; g.w_kblock = 0; g.n = H; g.k = ql;
         g.epi = EPI_SLAB; g.ksplit = so; g.slab = pf_slab; g.y = pf_x; g.ldy = H;
         LLMI_TRY(gemm2_launch(g, stream));
         g.w_kblock = 0;
@@ -716,7 +742,7 @@ struct Engine {
                 LLMI_TRY(prefill_attn_launch(pa, stream));
                 // o_proj + residual
                 g.a = pf_o; g.lda = ql; g.gamma = nullptr;
-                g.w = L.o; g.scales = L.o_s; g.n = H; g.k = ql; g.w_kblock = c.head_dim;  // head-major W_o
+                g.w = L.o; g.scales = L.o_s; g.n = H; g.k = ql;
                 g.epi = EPI_ADD; g.y = pf_x; g.ldy = H;
                 LLMI_TRY(gemm_launch(g, stream));
                 g.w_kblock = 0;
@@ -1055,6 +1081,13 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             case 4: return llmi::gemv_launch(g.down_args(l), g.stream);
             case 5: return llmi::gemv_launch(g.lm_args(), g.stream);
             case 7: return llmi::attn_oproj_fused_launch(g.attn_args_fused(l), g.o_args(l), &g.st->error, g.stream);
+            case 8: {  // ring layer (counters re-zeroed per launch)
+                LLMI_REQUIRE(g.ring_grid_n > 0, "time_kernel: the ring layer is not in use for this engine");
+                llmi::RingArgs ra = g.ring_args(l);
+                LLMI_HIP(hipMemsetAsync(ra.cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
+                return llmi::ring_layer_launch(ra, g.ring_grid_n, g.stream);
+            }
+            case 9: return llmi::attn_decode_launch(g.attn_args_ring(l), g.stream);
             case 6: {  // dataflow layer 0 (counters re-zeroed per launch)
                 LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
                 return llmi::layer_launch(g.layer_args(0), g.stream);
@@ -1067,7 +1100,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
                 return llmi::layer_launch_phases(L, which % 10, which % 10, g.stream);
             }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..7, 10..14 or 20..24");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..9, 10..14 or 20..24");
     };
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
@@ -1080,6 +1113,14 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             break;
         }
         case 2: b = (uint64_t)H * g.ql * ws + H * sc; break;
+        case 8: b = ((uint64_t)H * g.ql + 3ull * g.il * H) * ws + H * g.esz; break;
+        case 9: {
+            llmi::DecodeState hs;
+            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
+            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
+            b = (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb;
+            break;
+        }
         case 7: {  // attention (K/V read + slot write) + W_o
             llmi::DecodeState hs;
             LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));

@@ -156,6 +156,9 @@ struct AttnArgs {
     const long long* resid_fixed = nullptr;
     float resid_scale = 1.f;
     int hidden = 0;
+    // engine (ring layer): the last-arriving split workgroup of each head merges the
+    // head's partials and writes merge_out[h * D .. +D] (fp32); xacc must be null
+    float* merge_out = nullptr;
 };
 
 // Merge of the split partials fused into the o_proj, split by head: workgroup
@@ -197,6 +200,33 @@ __host__ __device__ __forceinline__ float from_fixed(long long v) {
 constexpr int kAttnChunk = 64;     // cached positions per workgroup (split-KV)
 size_t attn_workspace_bytes(int heads, int head_dim, int max_seq);
 int attn_decode_launch(const AttnArgs& a, hipStream_t s);
+
+// ------------------------------------------- ring layer (post-attention half)
+// o_proj + residual, RMSNorm + gate_up + SiLU*mul, down + residual as one
+// persistent launch with an LDS-DMA weight ring (ring.hip). fp16 weights,
+// row-major W_o [hidden, q_dim]; cnt: 2 * kPhaseCntWords u32, zero before launch.
+struct RingArgs {
+    const void* w_o = nullptr;
+    const void* w_gu = nullptr;     // [2 * inter, hidden] (gate rows, then up rows)
+    const void* w_d = nullptr;      // [hidden, inter]
+    const void* gamma = nullptr;    // ffn RMSNorm weight, fp16 [hidden]
+    float eps = 1e-5f;
+    int hidden = 0, q_dim = 0, inter = 0;
+    const float* attn = nullptr;    // merged attention output, fp32 [q_dim]
+    const long long* resid = nullptr;  // layer input residual (int64 fixed point)
+    int resid_keep = 1;
+    long long* xmid = nullptr;      // mid-layer residual (published in-launch)
+    float* act = nullptr;           // silu(g) * u (published in-launch)
+    long long* resid_out = nullptr; // layer output residual
+    float* x_out = nullptr;         // optional fp32 copy of xmid (workgroup 0)
+    unsigned* cnt = nullptr;
+    int* err = nullptr;
+    unsigned long long* stamps = nullptr;  // debug timeline (WgStamp + marks 5..7)
+};
+size_t ring_lds_bytes(const RingArgs& a);
+int ring_grid(int device);
+int ring_check(const RingArgs& a, int device);
+int ring_layer_launch(const RingArgs& a, int grid, hipStream_t s);
 
 // ------------------------------------------------ dataflow decode layer
 // One launch per layer: q/k/v GEMV, attention, merge + o_proj, gate_up, down

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=2048)
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--out", default="")
+    ap.add_argument("--ring-grid", type=int, default=256, help="workgroups of the ring layer (CUs)")
     a = ap.parse_args()
     lib = _lib.lib()
     cfg = preset("llama2-7b", layers=a.layers, max_seq=a.ctx)
@@ -51,16 +52,27 @@ def main():
             lib.llmi_memcpy(buf, zero.ctypes.data_as(C.c_void_p), C.c_size_t(nbytes), 0)
             e.time_kernel(k, 1)
             lib.llmi_memcpy(host.ctypes.data_as(C.c_void_p), buf, C.c_size_t(nbytes), 1)
-            v = host[host[:, 0] > 0].astype(np.int64)
+            rows = host[: a.ring_grid] if k == "ring" else host
+            v = rows[rows[:, 0] > 0].astype(np.int64)
             t0 = v[:, 0].min()
             st = (v[:, 0] - t0) / 100.0
             en = (v[:, 3] - t0) / 100.0
             r = {"wgs": int(len(v)), "span_us": round(float(en.max()), 2), "start_q": q(st), "dur_q": q(en - st),
                  "end_q": q(en), "cus": int(len(np.unique(v[:, 4])))}
-            for m in (1, 2):
+            for m in (1, 2, 5, 6, 7):
                 sel = v[:, m] > 0
                 if sel.any():
                     r[f"mark{m}_q"] = q((v[sel, m] - t0) / 100.0)
+            if k == "ring":  # per-piece cadence of workgroup 0: {issued, published, consumed}
+                nwg = a.ring_grid
+                pc = host[nwg:nwg + 1000].reshape(-1)[: 3 * 2000].reshape(-1, 3).astype(np.int64)
+                pc = pc[pc[:, 0] > 0]
+                if len(pc):
+                    rel = (pc - t0) / 100.0
+                    r["wg0_pieces"] = len(pc)
+                    r["wg0_issue_us"] = [round(float(x), 2) for x in rel[:, 0][::8]]
+                    r["wg0_land_minus_issue_q"] = q(rel[:, 1] - rel[:, 0])
+                    r["wg0_consume_minus_publish_q"] = q(rel[:, 2] - rel[:, 1])
             res[k] = r
             print(k, json.dumps(r), flush=True)
         lib.llmi_engine_debug_stamps(e._h, None)
