@@ -75,10 +75,32 @@ __global__ __launch_bounds__(kThreads) void attn_decode_merge_kernel(AttnArgs a)
     float* o2 = smem + 2 * ns;  // [2][D]
     float* linv = o2 + 2 * D;
     const float* mlh = ws.ml + (size_t)h * ns * 2;
-    const float* oh = ws.o + (size_t)h * ns * D;
-    for (int sp = tid; sp < nact; sp += kThreads) {
-        m_s[sp] = Sc1IO::ld(mlh + 2 * sp);
-        l_s[sp] = Sc1IO::ld(mlh + 2 * sp + 1);
+    const int d = tid % D, half = tid / D;
+    const float* oh = ws.o + (size_t)h * ns * D + d;
+    // every partial load in one round (o-partials, then m / l), as in the o_proj merge
+    float ov[kMergeChunk];
+#pragma unroll
+    for (int i = 0; i < kMergeChunk; ++i) {
+        const int sp = half + 2 * i;
+        ov[i] = Sc1IO::ld(oh + (size_t)(sp < nact ? sp : 0) * D);
+    }
+    constexpr int kMlPer = kMaxSplits / kThreads;
+    float mr[kMlPer], lr[kMlPer];
+#pragma unroll
+    for (int i = 0; i < kMlPer; ++i) {
+        if (i * kThreads < nact) {
+            const int sp = min(tid + i * kThreads, nact - 1);
+            mr[i] = Sc1IO::ld(mlh + 2 * sp);
+            lr[i] = Sc1IO::ld(mlh + 2 * sp + 1);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kMlPer; ++i) {
+        const int sp = tid + i * kThreads;
+        if (i * kThreads < nact && sp < nact) {
+            m_s[sp] = mr[i];
+            l_s[sp] = lr[i];
+        }
     }
     __syncthreads();
     if (tid < kWave) {
@@ -95,9 +117,13 @@ __global__ __launch_bounds__(kThreads) void attn_decode_merge_kernel(AttnArgs a)
         if (tid == 0) *linv = 1.0f / lsum;
     }
     __syncthreads();
-    const int d = tid % D, half = tid / D;
     float O = 0.f;
-    for (int sp = half; sp < nact; sp += 2) O = fmaf(Sc1IO::ld(oh + (size_t)sp * D + d), m_s[sp], O);
+#pragma unroll
+    for (int i = 0; i < kMergeChunk; ++i) {
+        const int sp = half + 2 * i;
+        O = fmaf(sp < nact ? ov[i] : 0.f, sp < nact ? m_s[sp] : 0.f, O);
+    }
+    for (int sp = half + 2 * kMergeChunk; sp < nact; sp += 2) O = fmaf(Sc1IO::ld(oh + (size_t)sp * D), m_s[sp], O);
     o2[half * D + d] = O;
     __syncthreads();
     if (tid < D) a.merge_out[(size_t)h * D + tid] = (o2[tid] + o2[D + tid]) * *linv;

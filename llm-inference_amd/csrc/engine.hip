@@ -274,7 +274,9 @@ struct Engine {
             //               (attn.hip; measured 21.8 vs 19.8 us for the two launches at ctx 2048)
             //               LLMI_FUSED=4: ring layer (ring.hip): attention merges in-kernel, then
             //               o_proj + gate_up + down as one persistent launch with an LDS-DMA weight ring
-            fuse_mode = !env ? 0 : env[0] == '1' ? 1 : env[0] == '2' ? 2 : env[0] == '3' ? 3 : env[0] == '4' ? 4 : 0;
+            //               LLMI_FUSED=5: attention merges in-kernel (last arriver), o_proj as a row GEMV
+            fuse_mode = !env ? 0 : (env[0] >= '1' && env[0] <= '5') ? env[0] - '0' : 0;
+            if (fuse_mode == 5 && (c.tp_world != 1 || grouped)) fuse_mode = 0;
             if (fuse_mode == 4) {
                 ring_grid_n = ring_grid(device);
                 if (wdt != LLMI_F16 || c.tp_world != 1 || grouped || ring_check(ring_args(0), device) != LLMI_OK)
@@ -391,7 +393,7 @@ struct Engine {
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
         a.grid = grid_qkv;
-        if (fuse_mode == 3) {  // the fused attention + o_proj adds into xacc from its first workgroup on:
+        if (fuse_mode == 3 || fuse_mode == 5) {  // o_proj adds into xacc from its first workgroup on:
             a.seed_src = res[l % 2]; a.seed_dst = xacc; a.seed_n = c.hidden;  // seed it here
             a.seed_keep = c.tp_rank == 0 ? 1 : 0;                               // (rank 0 carries the residual)
         }
@@ -401,6 +403,15 @@ struct Engine {
         AttnArgs a = attn_args(l);
         a.xacc = nullptr;
         a.merge_out = attn_out;  // merged per head in-kernel; the ring layer's o_proj input
+        return a;
+    }
+    GemvArgs o_gemv_args(int l) const {  // o_proj over whole rows of row-major W_o: xacc += W_o attn
+        const Layer& L = layers[l];
+        GemvArgs a;
+        a.stamps = dbg_stamps;
+        a.w = L.o; a.scales = L.o_s; a.w_dtype = wdt;
+        a.n_rows = c.hidden; a.k = ql; a.x = attn_out;
+        a.epi = EPI_ATOMIC; a.yacc = xacc; a.ksplit = 1;
         return a;
     }
     RingArgs ring_args(int l) const {
@@ -516,6 +527,10 @@ struct Engine {
         LLMI_TRY(gemv_launch(qkv_args(l), stream));
         if (fuse_mode == 3) return attn_oproj_fused_launch(attn_args_fused(l), o_args(l), &st->error, stream);
         if (fuse_mode == 4) return attn_decode_launch(attn_args_ring(l), stream);
+        if (fuse_mode == 5) {  // merged attention, then o_proj as a row GEMV adding into xacc
+            LLMI_TRY(attn_decode_launch(attn_args_ring(l), stream));
+            return gemv_launch(o_gemv_args(l), stream);
+        }
         if (fuse_mode == 2) {
             const int rc = layer_launch_phases(layer_args(l), 1, 2, stream);
             if (rc != LLMI_EUNSUPPORTED) return rc;
@@ -1088,6 +1103,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
                 return llmi::ring_layer_launch(ra, g.ring_grid_n, g.stream);
             }
             case 9: return llmi::attn_decode_launch(g.attn_args_ring(l), g.stream);
+            case 15: return llmi::gemv_launch(g.o_gemv_args(l), g.stream);
             case 6: {  // dataflow layer 0 (counters re-zeroed per launch)
                 LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
                 return llmi::layer_launch(g.layer_args(0), g.stream);
@@ -1100,7 +1116,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
                 return llmi::layer_launch_phases(L, which % 10, which % 10, g.stream);
             }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..9, 10..14 or 20..24");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..9, 10..15 or 20..24");
     };
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
@@ -1112,7 +1128,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             b = (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb;
             break;
         }
-        case 2: b = (uint64_t)H * g.ql * ws + H * sc; break;
+        case 2: case 15: b = (uint64_t)H * g.ql * ws + H * sc; break;
         case 8: b = ((uint64_t)H * g.ql + 3ull * g.il * H) * ws + H * g.esz; break;
         case 9: {
             llmi::DecodeState hs;

@@ -110,7 +110,7 @@ class Engine:
     def stream(self) -> int:
         return _lib.lib().llmi_engine_stream(self._h) or 0
 
-    KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5, "layer": 6, "attn_o": 7, "ring": 8, "attn_merge": 9,
+    KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5, "layer": 6, "attn_o": 7, "ring": 8, "attn_merge": 9, "o_gemv": 15,
                "f_qkv": 10, "f_attn": 11, "f_o": 12, "f_gate_up": 13, "f_down": 14,
                "p_qkv": 20, "p_attn": 21, "p_o": 22, "p_gate_up": 23, "p_down": 24}
 

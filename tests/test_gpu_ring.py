@@ -1,4 +1,5 @@
-"""Ring layer (ring.hip, LLMI_FUSED=4) on the MI355X: attention with the in-kernel
+"""Ring layer (ring.hip, LLMI_FUSED=4) and merged attention + row-GEMV o_proj
+(LLMI_FUSED=5) on the MI355X. Ring: attention with the in-kernel
 merge, then o_proj + gate_up + down as one persistent launch fed by an LDS-DMA
 weight ring. Bars: the reference fixtures (tokens exact, logits within the
 north-star 1e-3; fp32-KV parity runs within 2e-6 like the five-launch path), and
@@ -36,37 +37,40 @@ def run(cfg, seed, prompt, n_new, mode, use_graph=True):
             os.environ["LLMI_FUSED"] = old
 
 
+@pytest.mark.parametrize("mode", ["4", "5"])
 @pytest.mark.parametrize("name,cfgname,over,kv", [
     ("tiny.npz", "tiny", {}, _lib.F32),
     ("f3_decode.npz", "llama2-7b", dict(layers=2, max_seq=64), _lib.F32),
     ("f3_decode.npz", "llama2-7b", dict(layers=2, max_seq=64), _lib.F16),
 ])
-def test_ring_matches_reference(name, cfgname, over, kv):
+def test_ring_matches_reference(name, cfgname, over, kv, mode):
     f = np.load(os.path.join(G, name))
     cfg = preset(cfgname, **over)
     cfg.kv_dtype = kv
     n = len(f["tokens"])
-    t, lg, _ = run(cfg, int(f["seed"]), f["prompt"], n, "4")
+    t, lg, _ = run(cfg, int(f["seed"]), f["prompt"], n, mode)
     np.testing.assert_array_equal(t, f["tokens"])
     r = rel(lg, f["last_logits"])
     print(f"{name} ring logits rel-L2 vs reference: {r:.3e}")
     assert r < (2e-6 if kv == _lib.F32 else 1e-3)
 
 
-def test_ring_eager_equals_graph_bitwise():
+@pytest.mark.parametrize("mode", ["4", "5"])
+def test_ring_eager_equals_graph_bitwise(mode):
     cfg = preset("llama2-7b", layers=2, max_seq=128)
     prompt = synth_prompt(0, 8, cfg.vocab)
-    tg, lg, hg = run(cfg, 0, prompt, 40, "4")
-    te, le, he = run(cfg, 0, prompt, 40, "4", use_graph=False)
+    tg, lg, hg = run(cfg, 0, prompt, 40, mode)
+    te, le, he = run(cfg, 0, prompt, 40, mode, use_graph=False)
     np.testing.assert_array_equal(tg, te)
     np.testing.assert_array_equal(lg, le)
     np.testing.assert_array_equal(hg, he)
 
 
-def test_ring_full_7b_matches_five_launches():
+@pytest.mark.parametrize("mode", ["4", "5"])
+def test_ring_full_7b_matches_five_launches(mode):
     cfg = preset("llama2-7b", max_seq=512)
     prompt = synth_prompt(0, 8, cfg.vocab)
-    tr, lr, _ = run(cfg, 0, prompt, 300, "4")
+    tr, lr, _ = run(cfg, 0, prompt, 300, mode)
     tu, lu, _ = run(cfg, 0, prompt, 300, "0")
     np.testing.assert_array_equal(tr, tu)
     r = rel(lr, lu)
