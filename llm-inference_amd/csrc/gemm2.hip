@@ -45,6 +45,22 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) const void* glb_ptr_t;
 
 __device__ __forceinline__ int swz(int b) { return b ^ (((b >> 9) & 1) << 5); }
+
+#ifndef LLMI_GEMM2_STAGES
+#define LLMI_GEMM2_STAGES 3
+#endif
+constexpr int kStages = LLMI_GEMM2_STAGES;  // LDS stages: kStages - 1 in flight while one is multiplied
+
+// 16-B LDS-DMA as inline asm (M0 saved/restored): hipcc neither counts it nor waits
+// for it, so the K-loop's counted vmcnt keeps kStages - 1 stages in flight across the
+// raw barrier (cdna_hip_programming.md §5 "Pipelining across barriers")
+__device__ __forceinline__ void glds16(const void* g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
 
 // SILU pairing (as gemm.hip): tile row tr of the B tile holds gate column
@@ -100,22 +116,20 @@ __global__ __launch_bounds__(kThreads) void gemm2_kernel(Gemm2Args a) {
         const int src = b_src_row(EPI, n0, b >> 7, a.pair_off);
         b_src[j] = reinterpret_cast<const char*>(a.w) + (size_t)src * ldb * 2 + (b & 127);
     }
+    const unsigned lds_base = (unsigned)(uintptr_t)lds;
     auto issue = [&](int stage, int kl) {
         const int k0 = k_begin + kl;
-        char* base = lds + stage * STAGE + w * 1024;  // wave-uniform DMA base
+        const unsigned base = __builtin_amdgcn_readfirstlane(lds_base + stage * STAGE + w * 1024);  // wave-uniform
         const size_t koff =
             (a.w_kblock ? (size_t)(k0 / a.w_kblock) * a.n * a.w_kblock + k0 % a.w_kblock : (size_t)k0) * 2;
 #pragma unroll
         for (int p = 0; p < P; ++p)
 #pragma unroll
-            for (int j = 0; j < A_GL; ++j)
-                __builtin_amdgcn_global_load_lds((glb_ptr_t)(a_src[p][j] + (size_t)k0 * 2),
-                                                 (lds_ptr_t)(base + p * A_BYTES + j * kThreads * 16), 16, 0, 0);
+            for (int j = 0; j < A_GL; ++j) glds16(a_src[p][j] + (size_t)k0 * 2, base + p * A_BYTES + j * kThreads * 16);
 #pragma unroll
-        for (int j = 0; j < B_GL; ++j)
-            __builtin_amdgcn_global_load_lds((glb_ptr_t)(b_src[j] + koff),
-                                             (lds_ptr_t)(base + P * A_BYTES + j * kThreads * 16), 16, 0, 0);
+        for (int j = 0; j < B_GL; ++j) glds16(b_src[j] + koff, base + P * A_BYTES + j * kThreads * 16);
     };
+    constexpr int GL = P * A_GL + B_GL;  // DMA instructions per stage per thread
 
     f4 acc[MI][4];
 #pragma unroll
@@ -125,14 +139,21 @@ __global__ __launch_bounds__(kThreads) void gemm2_kernel(Gemm2Args a) {
 
     const int fr = lane & 15, fq = lane >> 4;
     const int KT = K / kBK;
-    issue(0, 0);
+#pragma unroll
+    for (int st = 0; st < kStages - 1; ++st)
+        if (st < KT) issue(st, st * kBK);
     for (int kt = 0; kt < KT; ++kt) {
-        // stage kt landed (every wave's DMAs drained, then the barrier publishes them);
-        // every wave also finished reading stage kt - 1, which the next issue overwrites
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (kt + 1 < KT) issue((kt + 1) & 1, (kt + 1) * kBK);
-        const char* As = lds + (kt & 1) * STAGE;
+        // stage kt landed in every wave (counted vmcnt: later stages stay in flight), then
+        // the raw barrier publishes it; every wave has also finished reading stage kt - 1,
+        // whose buffer the next issue refills
+        if (kt + kStages - 2 < KT) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(GL * (kStages - 2)) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        if (kt + kStages - 1 < KT) issue((kt + kStages - 1) % kStages, (kt + kStages - 1) * kBK);
+        const char* As = lds + (kt % kStages) * STAGE;
         const char* Bs = As + P * A_BYTES;
 #pragma unroll
         for (int kk = 0; kk < kBK / 32; ++kk) {
@@ -250,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
 
 template <int BM, int P, int EPI>
 int launch3(const Gemm2Args& a, int grid, hipStream_t s) {
-    constexpr size_t lds = 2 * (size_t)(P * BM * kRowB + kBN * kRowB);
+    constexpr size_t lds = kStages * (size_t)(P * BM * kRowB + kBN * kRowB);
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm2_kernel<BM, P, EPI>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
