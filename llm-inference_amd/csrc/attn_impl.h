@@ -335,7 +335,19 @@ __device__ __forceinline__ void oproj_load_w(const OprojArgs& a, int h, int chun
         int row = row0 + grp + 16 * t;
         row = row < a.n_rows ? row : a.n_rows - 1;
         const size_t off = a.head_major ? ((size_t)h * a.n_rows + row) * D : (size_t)row * a.ldw + (size_t)h * D;
-        wr[t] = ld_w8<WT>(w + off + l16 * 8);
+        if constexpr (sizeof(WT) == 1 && NPL >= 2) {
+            // int8: 16-B loads, 8 lanes per 128-column head slice, the two halves of a
+            // 16-lane group on rows t = 2u and 2u + 1 (wr[u], u < NPL / 2)
+            if (t < NPL / 2) {
+                int r2 = row0 + grp + 16 * (2 * t + (l16 >> 3));
+                r2 = r2 < a.n_rows ? r2 : a.n_rows - 1;
+                const size_t off2 =
+                    a.head_major ? ((size_t)h * a.n_rows + r2) * D : (size_t)r2 * a.ldw + (size_t)h * D;
+                wr[t].v[0] = ld_nt16(w + off2 + (l16 & 7) * 16);
+            }
+        } else {
+            wr[t] = ld_w8<WT>(w + off + l16 * 8);
+        }
     }
 }
 
@@ -439,6 +451,21 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
     __syncthreads();
     }
 
+    if constexpr (sizeof(WT) == 1 && NPL >= 2) {
+        float x16[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x16[i] = o_s[(l16 & 7) * 16 + i];
+#pragma unroll
+        for (int u = 0; u < NPL / 2; ++u) {
+            const uint32_t q[4] = {wr[u].v[0].x, wr[u].v[0].y, wr[u].v[0].z, wr[u].v[0].w};
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc = fmaf((float)(int8_t)((q[i / 4] >> (8 * (i % 4))) & 0xff), x16[i], acc);
+#pragma unroll
+            for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+            if ((l16 & 7) == 0) y_s[grp + 16 * (2 * u + (l16 >> 3))] = acc;
+        }
+    } else {
     float xv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) xv[i] = o_s[l16 * 8 + i];
@@ -452,6 +479,7 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
 #pragma unroll
         for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
         if (l16 == 0) y_s[grp + 16 * t] = acc;
+    }
     }
     __syncthreads();
     if (tid < 16 * NPL) {

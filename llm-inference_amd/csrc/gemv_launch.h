@@ -24,23 +24,54 @@ __global__ __launch_bounds__(kThreads, LLMI_GEMV_MIN_WAVES) void gemv_kernel(Gem
     gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs, NoSync{});
 }
 
+// Workgroups of one instantiation that fit the chip at once (occupancy x CUs),
+// cached per instantiation and LDS size.
+inline int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+    }
+    return cus;
+}
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int U, bool XF>
+int launch_k(const GemvArgs& a, int grid, size_t lds, hipStream_t s) {
+    auto kern = gemv_kernel<WT, ROWS, EPI, NORM, GT, XPT, U, XF>;
+    // An automatic grid larger than what is resident leaves the excess workgroups to
+    // start only when early ones retire -- a second, latency-bound round at the tail
+    // (profiles/r01c: int8 13B q/k/v and down). Clamp it to the resident count
+    // (argmax grids stay: their partial count is fixed by gemv_grid for step_start).
+    if (EPI != EPI_ARGMAX && a.grid == 0) {
+        static size_t occ_lds = ~(size_t)0;
+        static int occ_blocks = 0;
+        if (lds != occ_lds) {
+            int n = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kern), kThreads, lds) !=
+                hipSuccess)
+                n = 0;
+            occ_blocks = n * device_cus();
+            occ_lds = lds;
+        }
+        const int S = (EPI == EPI_ATOMIC) ? a.ksplit : 1;
+        if (occ_blocks >= S && grid > occ_blocks) grid = occ_blocks / S * S;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
 template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int U, bool XF>
 int launch_u(const GemvArgs& a, int grid, hipStream_t s) {
     const int kl = (EPI == EPI_ATOMIC) ? a.k / a.ksplit : a.k;  // x extent one workgroup stages
     const size_t lds = gemv_lds_bytes(kl);
     const int k4 = kl / 4;
-    if (k4 <= 4 * kThreads)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 4, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k4 <= 5 * kThreads)  // 13B hidden (5120)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 5, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k4 <= 11 * kThreads)  // 7B inter (11008)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 11, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else if (k4 <= 14 * kThreads)  // 13B inter (13824)
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 14, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    else
-        hipLaunchKernelGGL((gemv_kernel<WT, ROWS, EPI, NORM, GT, 0, U, XF>), dim3(grid), dim3(kThreads), lds, s, a);
-    LLMI_HIP(hipGetLastError());
-    return LLMI_OK;
+    if (k4 <= 4 * kThreads) return launch_k<WT, ROWS, EPI, NORM, GT, 4, U, XF>(a, grid, lds, s);
+    if (k4 <= 5 * kThreads) return launch_k<WT, ROWS, EPI, NORM, GT, 5, U, XF>(a, grid, lds, s);    // 13B hidden
+    if (k4 <= 11 * kThreads) return launch_k<WT, ROWS, EPI, NORM, GT, 11, U, XF>(a, grid, lds, s);  // 7B inter
+    if (k4 <= 14 * kThreads) return launch_k<WT, ROWS, EPI, NORM, GT, 14, U, XF>(a, grid, lds, s);  // 13B inter
+    return launch_k<WT, ROWS, EPI, NORM, GT, 0, U, XF>(a, grid, lds, s);
 }
 
 // Loads in flight per wave: measured on MI355X (tools/tune_gemv.sh, profiles/):

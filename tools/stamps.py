@@ -34,9 +34,14 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--out", default="")
     ap.add_argument("--ring-grid", type=int, default=256, help="workgroups of the ring layer (CUs)")
+    ap.add_argument("--preset", default="llama2-7b")
+    ap.add_argument("--int8", action="store_true", help="int8 W8A16 weights (config 5)")
     a = ap.parse_args()
     lib = _lib.lib()
-    cfg = preset("llama2-7b", layers=a.layers, max_seq=a.ctx)
+    cfg = preset(a.preset, layers=a.layers, max_seq=a.ctx)
+    if a.int8:
+        import llmi
+        cfg.weight_dtype = llmi.I8
     buf = C.c_void_p()
     nbytes = MAXWG * 8 * 8
     assert lib.llmi_device_alloc(C.byref(buf), C.c_size_t(nbytes)) == 0
