@@ -215,10 +215,10 @@ struct RingArgs {
     const float* attn = nullptr;    // merged attention output, fp32 [q_dim]
     const long long* resid = nullptr;  // layer input residual (int64 fixed point)
     int resid_keep = 1;
-    long long* xmid = nullptr;      // mid-layer residual (published in-launch)
+    long long* xmid = nullptr;      // (unused: xmid is published in-launch as fp32 through x_out)
     float* act = nullptr;           // silu(g) * u (published in-launch)
     long long* resid_out = nullptr; // layer output residual
-    float* x_out = nullptr;         // optional fp32 copy of xmid (workgroup 0)
+    float* x_out = nullptr;         // fp32 xmid [hidden]: the in-launch all-gather buffer (= the engine's x)
     unsigned* cnt = nullptr;
     int* err = nullptr;
     unsigned long long* stamps = nullptr;  // debug timeline (WgStamp + marks 5..7)

@@ -35,14 +35,21 @@
 namespace llmi {
 namespace {
 
-constexpr int kThreads = 256;
+#ifndef LLMI_RING_LOADERS
+#define LLMI_RING_LOADERS 2
+#endif
 constexpr int kSlotElems = 4096;               // fp16 weights per ring slot
 constexpr int kSlotBytes = kSlotElems * 2;     // 8 KB
-constexpr int kSlots = 18;                     // ring depth (144 KB): x lives in the consumers' registers
-constexpr int kLoaders = 1;                    // wave 0
-constexpr int kConsumers = 3;                  // waves 1..3
+constexpr int kSlots = 16;                     // ring depth (128 KB); x lives in the consumers' registers
+constexpr int kXImgBytes = 4096 * 4;           // one fp32 chunk of x, staged once for all consumer waves
+constexpr int kLoaders = LLMI_RING_LOADERS;    // waves 0 .. kLoaders - 1: each streams every kLoaders-th piece
+constexpr int kConsumers = 3;                  // the next three waves
+constexpr int kThreads = 64 * (kLoaders + kConsumers);
+#ifndef LLMI_RING_PREFETCH
+#define LLMI_RING_PREFETCH 32  // pieces past the ring that idle consumers touch at each all-gather
+#endif
 #ifndef LLMI_RING_DEPTH
-#define LLMI_RING_DEPTH 7
+#define LLMI_RING_DEPTH 6
 #endif
 constexpr int kDepth = LLMI_RING_DEPTH;        // pieces in flight: 8 DMA instructions each, vmcnt <= 63
 constexpr int kMaxChunks = 1;                  // x registers: one 4096-chunk (8 x 2 float4 per lane)
@@ -172,6 +179,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     int* freew = full + 32;
     int* csync_ctr = freew + 32;  // consumer-wave barrier counter
     long long* xmid_loc = reinterpret_cast<long long*>(smem + kSlots * kSlotBytes + 512);  // <= 64 rows
+    float* ximg = reinterpret_cast<float*>(smem + kSlots * kSlotBytes + kFlagBytes);  // [4096] fp32
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nwg = gridDim.x, b = blockIdx.x;
@@ -182,6 +190,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     const Plan p = make_plan(a, b, nwg);
     const int S = p.s_o + p.s_g + p.s_d;
 
+    static_assert(kSlots % kLoaders == 0, "each loader keeps its own slots");
     if (threadIdx.x < kSlots) {
         full[threadIdx.x] = -1;
         freew[threadIdx.x] = -1;
@@ -295,51 +304,79 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
             __hip_atomic_fetch_add(cnt + (b & (kCntShards - 1)) * kCntStride, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
     };
+    // While the consumers wait at an all-gather the ring is full and the loader idles:
+    // consumer waves 1.. touch the pieces the loader will issue next (one dword per
+    // 128-B line), so HBM keeps streaming into L2 / the Infinity Cache and the loader's
+    // DMA finds them there once the ring drains. Results are folded into a value that
+    // is never stored (the loads must not be dropped).
+    auto prefetch = [&](int s0, int s1) {
+        if (cw == 0 || LLMI_RING_PREFETCH == 0) return;
+        constexpr int kB = 16;
+        unsigned acc = 0;
+        for (int base = s0 + (cw - 1) * kB; base < s1; base += (kConsumers - 1) * kB) {
+            unsigned v[kB];
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                const int sq = min(base + k, s1 - 1);
+                const Piece pc = piece(a, p, sq);
+                v[k] = *reinterpret_cast<const unsigned*>(pc.src + min(lane * 128, pc.len * 2 - 4));
+            }
+#pragma unroll
+            for (int k = 0; k < kB; ++k) acc ^= v[k];
+        }
+        if (acc == 0x9e3779b9u && lane == 64) a.err[0] |= 0;  // never true for lane < 64: keeps the loads
+    };
     // lane's elements of chunk c: c * 4096 + (i * 64 + lane) * 8 + [0, 8), as 2 float4 (zeros past K)
     auto elem0 = [&](int c, int i) { return c * kSlotElems + (i * 64 + lane) * 8; };
     float* part = reinterpret_cast<float*>(smem + kSlots * kSlotBytes + 1024);  // D partials [48 rows][kConsumers]
 
-    // ---- O: attn (fp32 [q_dim <= 4096], previous launch) into registers; rows of W_o
-    {
+    // x of one chunk for every consumer wave: staged once into the LDS image by all
+    // consumer threads, then each lane copies its 64 values into registers
+    const int ct = threadIdx.x - 64 * kLoaders;  // 0 .. 64 * kConsumers - 1
+    auto image_to_regs = [&](int k) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int e = elem0(0, i);
-            const bool in = e < a.q_dim;
-            const float4* src = reinterpret_cast<const float4*>(a.attn + (in ? e : 0));
+            const bool in = e < k;
+            const float4* src = reinterpret_cast<const float4*>(ximg + (in ? e : 0));
             xr[i][0] = in ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
             xr[i][1] = in ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+    };
+    // ---- O: attn (fp32 [q_dim <= 4096], previous launch) into registers; rows of W_o
+    {
+        for (int j = ct; j < a.q_dim / 4; j += 64 * kConsumers)
+            reinterpret_cast<float4*>(ximg)[j] = reinterpret_cast<const float4*>(a.attn)[j];
+        csync();
+        image_to_regs(a.q_dim);
         for (int r = cw; r < p.o_n; r += kConsumers) {
             const float acc = wave_sum(consume(r, a.q_dim));
             if (lane == 0) {
                 const int row = p.o_b + r;
                 const long long v = (a.resid_keep ? a.resid[row] : 0ll) + to_fixed(acc);
                 xmid_loc[r] = v;
-                Sc1IO::st_ll(a.xmid + row, v);
+                Sc1IO::st(a.x_out + row, from_fixed(v));  // the all-gather carries fp32 xmid (= x)
             }
         }
         publish(a.cnt);
         if (cw == 0) mark(1);
     }
     // ---- G: all-gather xmid into registers (x and sum x^2), gamma, gate/up pairs
+    prefetch(p.s_o + kSlots, min(p.s_o + kSlots + LLMI_RING_PREFETCH, S));
     gather_wait(a.cnt);
     if (cw == 0) mark(2);
     {
+        csync();  // every wave is done reading the image (O phase copy) before it is refilled
+        for (int j = ct; j < a.hidden / 4; j += 64 * kConsumers)
+            reinterpret_cast<float4*>(ximg)[j] = Sc1IO::ld4(reinterpret_cast<const float4*>(a.x_out) + j);
+        csync();
+        image_to_regs(a.hidden);
         float ss = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int e = elem0(0, i);
             const bool in = e < a.hidden;
-            const longlong2* f = reinterpret_cast<const longlong2*>(a.xmid + (in ? e : 0));
-            const longlong2 f0 = Sc1IO::ld_ll2(f), f1 = Sc1IO::ld_ll2(f + 1), f2 = Sc1IO::ld_ll2(f + 2),
-                            f3 = Sc1IO::ld_ll2(f + 3);
-            float4 v0 = make_float4(from_fixed(f0.x), from_fixed(f0.y), from_fixed(f1.x), from_fixed(f1.y));
-            float4 v1 = make_float4(from_fixed(f2.x), from_fixed(f2.y), from_fixed(f3.x), from_fixed(f3.y));
-            if (!in) v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (in && b == 0 && cw == 0 && a.x_out) {
-                reinterpret_cast<float4*>(a.x_out + e)[0] = v0;
-                reinterpret_cast<float4*>(a.x_out + e)[1] = v1;
-            }
+            const float4 v0 = xr[i][0], v1 = xr[i][1];
             ss += v0.x * v0.x + v0.y * v0.y + v0.z * v0.z + v0.w * v0.w;
             ss += v1.x * v1.x + v1.y * v1.y + v1.z * v1.z + v1.w * v1.w;
             const uint4 gu = *reinterpret_cast<const uint4*>(reinterpret_cast<const __half*>(a.gamma) + (in ? e : 0));
@@ -360,6 +397,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         if (cw == 0) mark(5);
     }
     // ---- D: all-gather act into registers, down rows, resid' = xmid + W_d act
+    prefetch(p.s_o + p.s_g + kSlots, min(p.s_o + p.s_g + kSlots + LLMI_RING_PREFETCH, S));
     gather_wait(a.cnt + kPhaseCntWords);
     if (cw == 0) mark(6);
     // chunk-owner: consumer wave cw takes chunk cw of every down row (x = that chunk of
@@ -396,7 +434,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
 
 size_t ring_lds_bytes(const RingArgs& a) {
     (void)a;
-    return (size_t)kSlots * kSlotBytes + kFlagBytes;
+    return (size_t)kSlots * kSlotBytes + kFlagBytes + kXImgBytes;
 }
 
 int ring_grid(int device) {
@@ -422,7 +460,7 @@ int ring_check(const RingArgs& a, int device) {
 }
 
 int ring_layer_launch(const RingArgs& a, int grid, hipStream_t s) {
-    LLMI_REQUIRE(a.w_o && a.w_gu && a.w_d && a.gamma && a.attn && a.resid && a.xmid && a.act && a.resid_out && a.cnt &&
+    LLMI_REQUIRE(a.w_o && a.w_gu && a.w_d && a.gamma && a.attn && a.resid && a.x_out && a.act && a.resid_out && a.cnt &&
                      a.err && grid > 0,
                  "ring: null argument");
     hipLaunchKernelGGL(ring_layer_kernel, dim3(grid), dim3(kThreads), ring_lds_bytes(a), s, a);

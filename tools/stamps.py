@@ -78,6 +78,7 @@ def main():
                     r["wg0_issue_us"] = [round(float(x), 2) for x in rel[:, 0][::8]]
                     r["wg0_land_minus_issue_q"] = q(rel[:, 1] - rel[:, 0])
                     r["wg0_consume_minus_publish_q"] = q(rel[:, 2] - rel[:, 1])
+                    r["wg0_table_us"] = [[round(float(x), 3) for x in row] for row in rel]
             res[k] = r
             print(k, json.dumps(r), flush=True)
         lib.llmi_engine_debug_stamps(e._h, None)
