@@ -199,6 +199,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_kernel(const float* qkv
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int QM = 64;  // query rows per workgroup
+__device__ __forceinline__ int vswz(int d) { return (d ^ (d >> 3)) & 7; }  // Vt row d's 16-B chunk XOR
 constexpr int KB = 64;  // keys per block
 
 template <int P>
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
                                                                      _Float16* out_hi, _Float16* out_lo, int ldo) {
     __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 + D * KB * 2 + 4 * P * 16 * KB * 2];
     char* Ks = smem;                 // [key][256 B], chunk ^= key & 15
-    char* Vt = smem + KB * D * 2;    // [dim][128 B], chunk ^= dim & 7
+    char* Vt = smem + KB * D * 2;    // [dim][128 B], chunk ^= vswz(dim)
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int fr = lane & 15, fq = lane >> 4;
     char* Pw = Vt + D * KB * 2 + w * P * 16 * KB * 2;  // this wave's [P][16][128 B], chunk ^= row & 7
@@ -246,12 +247,20 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
     // staging: thread t moves 16 B (8 dims) of key rows t / 16 + 16 i, chunk t % 16
     const int sr = t >> 4, sc = t & 15;
     uint4 kreg[4], vreg[4];
+    // K: key rows sr + 16 i (i < 4); V: key PAIRS 2 (sr + 16 i), +1 (i < 2), so each
+    // transposed store writes two keys of one dim (4 B) -- half the stores of a
+    // per-key transpose, and the Vt chunk swizzle (d ^ d >> 3) & 7 spreads them over the banks
     auto gload = [&](int kb) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int key = min(kb * KB + sr + 16 * i, kend - 1);
             kreg[i] = *reinterpret_cast<const uint4*>(kc + (size_t)key * D + sc * 8);
-            vreg[i] = *reinterpret_cast<const uint4*>(vc + (size_t)key * D + sc * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int k0 = kb * KB + 2 * (sr + 16 * i);
+            vreg[2 * i] = *reinterpret_cast<const uint4*>(vc + (size_t)min(k0, kend - 1) * D + sc * 8);
+            vreg[2 * i + 1] = *reinterpret_cast<const uint4*>(vc + (size_t)min(k0 + 1, kend - 1) * D + sc * 8);
         }
     };
     auto lstore = [&]() {
@@ -259,11 +268,17 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
         for (int i = 0; i < 4; ++i) {
             const int r = sr + 16 * i;
             *reinterpret_cast<uint4*>(Ks + r * 256 + ((sc ^ (r & 15)) << 4)) = kreg[i];
-            const _Float16* hv = reinterpret_cast<const _Float16*>(&vreg[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int r0 = 2 * (sr + 16 * i);
+            const _Float16* h0 = reinterpret_cast<const _Float16*>(&vreg[2 * i]);
+            const _Float16* h1 = reinterpret_cast<const _Float16*>(&vreg[2 * i + 1]);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int d = sc * 8 + e;
-                *reinterpret_cast<_Float16*>(Vt + d * 128 + (((r >> 3) ^ (d & 7)) << 4) + (r & 7) * 2) = hv[e];
+                typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<h2*>(Vt + d * 128 + (((r0 >> 3) ^ vswz(d)) << 4) + (r0 & 7) * 2) = h2{h0[e], h1[e]};
             }
         }
     };
@@ -357,7 +372,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
 #pragma unroll
             for (int jt = 0; jt < 8; ++jt) {
                 const int d = 16 * jt + fr;
-                const h8 bv = *reinterpret_cast<const h8*>(Vt + d * 128 + (((4 * kk + fq) ^ (d & 7)) << 4));
+                const h8 bv = *reinterpret_cast<const h8*>(Vt + d * 128 + (((4 * kk + fq) ^ vswz(d)) << 4));
 #pragma unroll
                 for (int p = 0; p < P; ++p) o[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[p], bv, o[jt], 0, 0, 0);
             }
