@@ -17,6 +17,9 @@ constexpr int kWavesPerBlock = kThreads / kWave;
 #ifndef LLMI_GEMV_ROWS
 #define LLMI_GEMV_ROWS 2
 #endif
+#ifndef LLMI_I8_PIPE
+#define LLMI_I8_PIPE 0  // software-pipelined int8 gate_up stream (measured: 30.7 vs 28.2 us once grids are clamped to residency)
+#endif
 #ifndef LLMI_GEMV_PIPE16
 #define LLMI_GEMV_PIPE16 0  // bit EPI: software-pipelined fp16 stream for that epilogue
 #endif
@@ -268,7 +271,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
     // item's loads are issued before the current item's convert + FMA work, across
     // row-group boundaries too; two register buffers, manually unrolled by 2. The
     // item after the last one re-loads the last item (a cache hit, never used).
-    constexpr bool PIPE = (sizeof(WT) == 1 && kUnroll <= 5 && EPI == EPI_SILU_MUL)  // measured: a win on
+    constexpr bool PIPE = (LLMI_I8_PIPE && sizeof(WT) == 1 && kUnroll <= 5 && EPI == EPI_SILU_MUL)  // measured: a win on
     // gate_up only (q/k/v and down lost occupancy to the second buffer, tools/int8_probe.py)
                           || (sizeof(WT) == 2 && ((LLMI_GEMV_PIPE16 >> EPI) & 1));
     if constexpr (PIPE) {
