@@ -271,8 +271,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
     // item's loads are issued before the current item's convert + FMA work, across
     // row-group boundaries too; two register buffers, manually unrolled by 2. The
     // item after the last one re-loads the last item (a cache hit, never used).
-    constexpr bool PIPE = (LLMI_I8_PIPE && sizeof(WT) == 1 && kUnroll <= 5 && EPI == EPI_SILU_MUL)  // measured: a win on
-    // gate_up only (q/k/v and down lost occupancy to the second buffer, tools/int8_probe.py)
+    // LLMI_I8_PIPE: bit EPI enables it for that epilogue (4 = gate_up only)
+    constexpr bool PIPE = (sizeof(WT) == 1 && kUnroll <= 5 && ((LLMI_I8_PIPE >> EPI) & 1))
                           || (sizeof(WT) == 2 && ((LLMI_GEMV_PIPE16 >> EPI) & 1));
     if constexpr (PIPE) {
         constexpr int B = kWave * kUnroll;

@@ -15,8 +15,13 @@ namespace gemv_detail {
 #define LLMI_GEMV_MIN_WAVES 1  // min waves per SIMD (launch-bounds 2nd arg): caps VGPRs
 #endif
 
+#ifndef LLMI_GEMV_MIN_WAVES_I8
+#define LLMI_GEMV_MIN_WAVES_I8 LLMI_GEMV_MIN_WAVES  // int8: 16 weights per load need 4 float4 of x each
+#endif
+template <typename WT> constexpr int min_waves() { return sizeof(WT) == 1 ? LLMI_GEMV_MIN_WAVES_I8 : LLMI_GEMV_MIN_WAVES; }
+
 template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX>
-__global__ __launch_bounds__(kThreads, LLMI_GEMV_MIN_WAVES) void gemv_kernel(GemvArgs a) {
+__global__ __launch_bounds__(kThreads, min_waves<WT>()) void gemv_kernel(GemvArgs a) {
     // all LDS in one 16-B aligned dynamic region (cdna_hip_programming.md G17):
     // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
