@@ -108,6 +108,51 @@ int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_d
  * greedy argmax over logits[n]; ties -> lowest index. out_id: device int32. */
 int llmi_argmax(const float* logits, int n, int32_t* out_id, llmi_stream_t stream);
 
+/* ---- context-phase (prefill) operators of the reference's unfused attention layer
+ * (LLaMAContextAttentionLayer::forward, context_attention.cpp:108-161). The engine's
+ * llmi_engine_prefill fuses them; these are the per-launcher equivalents. dtype is
+ * LLMI_F32 or LLMI_F16 for every tensor of a call (fp32 arithmetic); integer arrays
+ * are device int32. Layouts are the reference's. */
+
+/* launchAddFusedQKVBiasTransposeAndRoPE (src/kernels/qkv_bias_and_RoPE.h:26-36,
+ * .cu:49-144), Llama (no bias): qkv [num_tokens, (heads + 2 kv_heads) * d] ->
+ * q [batch, heads, seq_len, d], k, v [batch, kv_heads, seq_len, d]; token i goes to
+ * padded position i + padding_offset[i]; q and k are rotated at position
+ * history_length[b] + s (s = the token's index in its sequence), pairs (i, i + d/2),
+ * with llmi_rope_decode's angle arithmetic. Two deliberate differences from the
+ * reference kernel (bugs there): v is written (the reference leaves v_buf unset) and
+ * the position is per sequence (the reference adds the packed token index, which is
+ * the same thing at batch 1). */
+int llmi_rope_qkv_prefill(const void* qkv, void* q, void* k, void* v, int dtype, const int32_t* padding_offset,
+                          const int32_t* history_length, int num_tokens, int batch, int seq_len, int heads,
+                          int kv_heads, int head_dim, float rope_base, llmi_stream_t stream);
+
+/* launchConcatKVCache (src/kernels/concat_past_kv.h:11-18, .cu:16-143): k_src, v_src
+ * [batch, kv_heads, max_q_len, d] -> caches [layers, batch, kv_heads, max_seq, d] at
+ * slots history_length[b] + t for t < cur_query_length[b] of layer `layer`. */
+int llmi_kv_append(const void* k_src, const void* v_src, int dtype, int layer, const int32_t* cur_query_length,
+                   const int32_t* history_length, int batch, int kv_heads, int max_q_len, int head_dim, int max_seq,
+                   void* k_cache, void* v_cache, llmi_stream_t stream);
+
+/* launchBuildCausalMasks (src/kernels/build_causal_mask.h:8-11, .cu:4-45): mask
+ * [batch, max_q_len, max_k_len] = 1 where q < q_lens[b], k < k_lens[b] and
+ * k_lens[b] - q_lens[b] <= k <= q + k_lens[b] - q_lens[b], else 0. */
+int llmi_causal_mask(void* mask, int dtype, const int32_t* q_lens, const int32_t* k_lens, int batch,
+                     int max_q_len, int max_k_len, llmi_stream_t stream);
+
+/* launchScaleMaskAndSoftmax (src/kernels/attn_softmax_kernel.h:8-12, .cu:79-174):
+ * score[b, h, q, :] = softmax(scale * qk[b, h, q, :] + (1 - mask[b, q, :]) * -10000)
+ * normalised by 1 / (sum + 1e-6) as the reference; qk, score [batch, heads, q_len,
+ * k_len], mask [batch, q_len, k_len]. score may alias qk. */
+int llmi_masked_softmax(const void* qk, const void* mask, void* score, int dtype, int batch, int heads, int q_len,
+                        int k_len, float scale, llmi_stream_t stream);
+
+/* launchTransposeOutRemovePadding (src/kernels/fused_transpose_and_remv_pad.h:7-9,
+ * .cu:17-75): src [batch, heads, seq_len, d] -> dst [num_tokens, heads * d], token i
+ * read from padded position i + padding_offset[i]. */
+int llmi_transpose_remove_pad(const void* src, const int32_t* padding_offset, void* dst, int dtype, int num_tokens,
+                              int batch, int seq_len, int heads, int head_dim, llmi_stream_t stream);
+
 /* Synthetic-weight generator (replaces LlamaLayerWeight::loadWeights() dummy
  * path, src/weights/llama/layer_weights.cc:69-146). Fills the [rows, cols]
  * slice (row0, col0) of a logical [*, ld] tensor `tid` with llmi-prng-v1

@@ -104,6 +104,36 @@ int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_d
     return attn_decode_launch(a, STREAM(stream));
 }
 
+int llmi_rope_qkv_prefill(const void* qkv, void* q, void* k, void* v, int dtype, const int32_t* padding_offset,
+                          const int32_t* history_length, int num_tokens, int batch, int seq_len, int heads,
+                          int kv_heads, int head_dim, float rope_base, llmi_stream_t stream) {
+    return rope_qkv_prefill_launch(qkv, q, k, v, dtype, padding_offset, history_length, num_tokens, batch, seq_len,
+                                   heads, kv_heads, head_dim, rope_base, STREAM(stream));
+}
+
+int llmi_kv_append(const void* k_src, const void* v_src, int dtype, int layer, const int32_t* cur_query_length,
+                   const int32_t* history_length, int batch, int kv_heads, int max_q_len, int head_dim, int max_seq,
+                   void* k_cache, void* v_cache, llmi_stream_t stream) {
+    return kv_append_launch(k_src, v_src, dtype, layer, cur_query_length, history_length, batch, kv_heads, max_q_len,
+                            head_dim, max_seq, k_cache, v_cache, STREAM(stream));
+}
+
+int llmi_causal_mask(void* mask, int dtype, const int32_t* q_lens, const int32_t* k_lens, int batch,
+                     int max_q_len, int max_k_len, llmi_stream_t stream) {
+    return causal_mask_launch(mask, dtype, q_lens, k_lens, batch, max_q_len, max_k_len, STREAM(stream));
+}
+
+int llmi_masked_softmax(const void* qk, const void* mask, void* score, int dtype, int batch, int heads, int q_len,
+                        int k_len, float scale, llmi_stream_t stream) {
+    return masked_softmax_launch(qk, mask, score, dtype, batch, heads, q_len, k_len, scale, STREAM(stream));
+}
+
+int llmi_transpose_remove_pad(const void* src, const int32_t* padding_offset, void* dst, int dtype, int num_tokens,
+                              int batch, int seq_len, int heads, int head_dim, llmi_stream_t stream) {
+    return transpose_remove_pad_launch(src, padding_offset, dst, dtype, num_tokens, batch, seq_len, heads, head_dim,
+                                       STREAM(stream));
+}
+
 int llmi_argmax(const float* logits, int n, int32_t* out_id, llmi_stream_t stream) {
     // 256 x 8 B of scratch for the partial keys: a per-process device buffer
     static unsigned long long* scratch = nullptr;

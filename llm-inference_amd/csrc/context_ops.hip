@@ -1,0 +1,233 @@
+// Context-phase (prefill) operators of the reference's unfused attention layer,
+// as standalone launches for the operator API (SURVEY.md §8 a15 and §8b's export
+// set): LLaMAContextAttentionLayer::forward (context_attention.cpp:108-161) calls
+// launchAddFusedQKVBiasTransposeAndRoPE -> launchConcatKVCache -> QK^T ->
+// launchBuildCausalMasks / launchScaleMaskAndSoftmax -> PV ->
+// launchTransposeOutRemovePadding. The engine's prefill fuses all of it
+// (prefill.hip: RoPE + KV write, then one MFMA flash-attention kernel with the
+// causal test key <= p0 + row); these launches exist so a caller of the
+// reference's launchers finds each one with the same layouts and meaning.
+//
+// All are memory-bound element moves or row reductions (fp32 arithmetic, T = float
+// or __half storage); roofline HBM, bytes = what they read + write.
+#include <cfloat>
+
+#include "kernels.h"
+
+namespace llmi {
+namespace {
+
+template <typename T> __device__ __forceinline__ float ldf(const T* p) { return (float)*p; }
+template <> __device__ __forceinline__ float ldf<__half>(const __half* p) { return __half2float(*p); }
+template <typename T> __device__ __forceinline__ void stf(T* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void stf<__half>(__half* p, float v) { *p = __float2half(v); }
+
+// BuildCausalMasksConsideringContextPastKV (build_causal_mask.cu:4-45): one workgroup
+// per sequence; 1 where q < q_len, k < k_len and k_len - q_len <= k <= q + (k_len - q_len).
+template <typename T>
+__global__ void causal_mask_kernel(T* mask, const int* q_lens, const int* k_lens, int max_q, int max_k) {
+    const int qlen = q_lens[blockIdx.x], klen = k_lens[blockIdx.x];
+    T* m = mask + (size_t)blockIdx.x * max_q * max_k;
+    for (int o = threadIdx.x; o < max_q * max_k; o += blockDim.x) {
+        const int q = o / max_k, k = o % max_k;
+        const bool one = q < qlen && k < klen && k <= q + (klen - qlen) && k >= klen - qlen;
+        stf(m + o, one ? 1.f : 0.f);
+    }
+}
+
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_xor(v, off, kWave);
+        v = is_max ? fmaxf(v, o) : v + o;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    float r = sh[0];
+    for (int i = 1; i < nw; ++i) r = is_max ? fmaxf(r, sh[i]) : r + sh[i];
+    return r;
+}
+
+// ScaleMaskAndSoftmax (attn_softmax_kernel.cu:79-174): one workgroup per (q row, batch,
+// head); x = scale * qk + (1 - mask) * -10000, p = exp(x - max) / (sum + 1e-6). The row
+// max is the true maximum (the reference seeds its running max with FLT_MIN, which only
+// differs when every x of a row is below the exp underflow range).
+template <typename T>
+__global__ void masked_softmax_kernel(const T* qk, const T* mask, T* score, int heads, int q_len, int k_len,
+                                      float scale) {
+    __shared__ float sh[16];
+    const int q = blockIdx.x, b = blockIdx.y, h = blockIdx.z;
+    const size_t row = (((size_t)b * heads + h) * q_len + q) * k_len;
+    const T* mrow = mask + ((size_t)b * q_len + q) * k_len;
+    auto x_at = [&](int k) { return scale * ldf(qk + row + k) + (1.f - ldf(mrow + k)) * -10000.0f; };
+    float mx = -FLT_MAX;
+    for (int k = threadIdx.x; k < k_len; k += blockDim.x) mx = fmaxf(mx, x_at(k));
+    mx = block_reduce(mx, sh, true);
+    float s = 0.f;
+    for (int k = threadIdx.x; k < k_len; k += blockDim.x) s += expf(x_at(k) - mx);
+    s = block_reduce(s, sh, false);
+    const float inv = 1.f / (s + 1e-6f);
+    for (int k = threadIdx.x; k < k_len; k += blockDim.x) stf(score + row + k, expf(x_at(k) - mx) * inv);
+}
+
+// append_key_cache / append_value_cache (concat_past_kv.cu:16-91): grid (max_q_len,
+// batch, 2 * kv_heads) -- k heads then v heads in one launch; block = head_dim.
+template <typename T>
+__global__ void kv_append_kernel(const T* k_src, const T* v_src, T* k_dst, T* v_dst, const int* cur_q,
+                                 const int* hist, int kv_heads, int d, int max_q, int max_seq) {
+    const int t = blockIdx.x, b = blockIdx.y, hz = blockIdx.z;
+    if (t >= cur_q[b]) return;
+    const bool is_v = hz >= kv_heads;
+    const int h = is_v ? hz - kv_heads : hz;
+    const T* src = (is_v ? v_src : k_src) + (((size_t)b * kv_heads + h) * max_q + t) * d;
+    T* dst = (is_v ? v_dst : k_dst) + (((size_t)b * kv_heads + h) * max_seq + hist[b] + t) * d;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) dst[i] = src[i];
+}
+
+// fused_transpose_reshape_remv_pad (fused_transpose_and_remv_pad.cu:17-47): token i
+// reads padded position i + padding_offset[i] of src [batch, heads, seq_len, d].
+template <typename T>
+__global__ void transpose_remove_pad_kernel(const T* src, T* dst, const int* po, int seq_len, int heads, int d) {
+    const int i = blockIdx.x;
+    const int p = i + po[i], b = p / seq_len, s = p % seq_len;
+    const T* sb = src + (size_t)b * heads * seq_len * d + (size_t)s * d;
+    T* o = dst + (size_t)i * heads * d;
+    for (int e = threadIdx.x; e < heads * d; e += blockDim.x) o[e] = sb[(size_t)(e / d) * seq_len * d + e % d];
+}
+
+// angle of pair i at position pos: llmi_rope_decode's arithmetic (ops.hip), HF's
+// inv_freq = 1 / base^(2i/d) with the power correctly rounded (modeling_llama.py:123-146)
+__device__ __forceinline__ void rope_angle(int pos, int i, int d, float base, float* c, float* s) {
+    const float p = (float)pow((double)base, (double)(2 * i) / (double)d);
+    const float ang = __fmul_rn((float)pos, __fdiv_rn(1.0f, p));
+    double sd, cd;
+    sincos((double)ang, &sd, &cd);
+    *c = (float)cd;
+    *s = (float)sd;
+}
+
+// add_fusedQKV_bias_transpose_kernel (qkv_bias_and_RoPE.cu:49-144), Llama (no bias):
+// grid (num_tokens, heads), block d. Threads < d/2 rotate the pair (i, i + d/2) of q
+// (and of k for head < kv_heads); every thread of a head < kv_heads copies v.
+template <typename T>
+__global__ void rope_qkv_prefill_kernel(const T* qkv, T* q_buf, T* k_buf, T* v_buf, const int* po, const int* hist,
+                                        int seq_len, int heads, int kv_heads, int d, float base) {
+    const int tok = blockIdx.x, h = blockIdx.y, t = threadIdx.x;
+    const int p = tok + po[tok], b = p / seq_len, s = p % seq_len;
+    const T* row = qkv + (size_t)tok * (heads + 2 * kv_heads) * d;
+    const size_t qo = (((size_t)b * heads + h) * seq_len + s) * d;
+    const size_t ko = (((size_t)b * kv_heads + h) * seq_len + s) * d;
+    if (t < d / 2) {
+        float c, sn;
+        rope_angle(hist[b] + s, t, d, base, &c, &sn);
+        const T* qh = row + (size_t)h * d;
+        const float q0 = ldf(qh + t), q1 = ldf(qh + t + d / 2);
+        stf(q_buf + qo + t, q0 * c - q1 * sn);
+        stf(q_buf + qo + t + d / 2, q1 * c + q0 * sn);
+        if (h < kv_heads) {
+            const T* kh = row + (size_t)(heads + h) * d;
+            const float k0 = ldf(kh + t), k1 = ldf(kh + t + d / 2);
+            stf(k_buf + ko + t, k0 * c - k1 * sn);
+            stf(k_buf + ko + t + d / 2, k1 * c + k0 * sn);
+        }
+    }
+    if (h < kv_heads && t < d) v_buf[ko + t] = row[(size_t)(heads + kv_heads + h) * d + t];
+}
+
+bool fp_dtype(int dt) { return dt == LLMI_F32 || dt == LLMI_F16; }
+
+}  // namespace
+
+int causal_mask_launch(void* mask, int dtype, const int* q_lens, const int* k_lens, int batch, int max_q, int max_k,
+                       hipStream_t s) {
+    LLMI_REQUIRE(mask && q_lens && k_lens && batch > 0 && max_q > 0 && max_k > 0, "causal_mask: bad arguments");
+    LLMI_REQUIRE(fp_dtype(dtype), "causal_mask: dtype must be f32 or f16");
+    if (dtype == LLMI_F32)
+        hipLaunchKernelGGL(causal_mask_kernel<float>, dim3(batch), dim3(256), 0, s, (float*)mask, q_lens, k_lens, max_q,
+                           max_k);
+    else
+        hipLaunchKernelGGL(causal_mask_kernel<__half>, dim3(batch), dim3(256), 0, s, (__half*)mask, q_lens, k_lens,
+                           max_q, max_k);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int masked_softmax_launch(const void* qk, const void* mask, void* score, int dtype, int batch, int heads, int q_len,
+                          int k_len, float scale, hipStream_t s) {
+    LLMI_REQUIRE(qk && mask && score && batch > 0 && heads > 0 && q_len > 0 && k_len > 0,
+                 "masked_softmax: bad arguments");
+    LLMI_REQUIRE(batch <= 65535 && heads <= 65535, "masked_softmax: batch and heads must be <= 65535");
+    LLMI_REQUIRE(fp_dtype(dtype), "masked_softmax: dtype must be f32 or f16");
+    const dim3 grid(q_len, batch, heads);
+    if (dtype == LLMI_F32)
+        hipLaunchKernelGGL(masked_softmax_kernel<float>, grid, dim3(256), 0, s, (const float*)qk, (const float*)mask,
+                           (float*)score, heads, q_len, k_len, scale);
+    else
+        hipLaunchKernelGGL(masked_softmax_kernel<__half>, grid, dim3(256), 0, s, (const __half*)qk,
+                           (const __half*)mask, (__half*)score, heads, q_len, k_len, scale);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int kv_append_launch(const void* k_src, const void* v_src, int dtype, int layer, const int* cur_q, const int* hist,
+                     int batch, int kv_heads, int max_q, int d, int max_seq, void* k_cache, void* v_cache,
+                     hipStream_t s) {
+    LLMI_REQUIRE(k_src && v_src && k_cache && v_cache && cur_q && hist, "kv_append: null pointer");
+    LLMI_REQUIRE(layer >= 0 && batch > 0 && kv_heads > 0 && max_q > 0 && d > 0 && d <= 1024 && max_seq > 0,
+                 "kv_append: bad shape");
+    LLMI_REQUIRE(batch <= 65535 && 2 * kv_heads <= 65535, "kv_append: batch / kv_heads too large");
+    LLMI_REQUIRE(fp_dtype(dtype), "kv_append: dtype must be f32 or f16");
+    // layer offset as the reference's (concat_past_kv.cu:122): layer * batch * kv_heads * max_seq * d
+    const size_t off = (size_t)layer * batch * kv_heads * max_seq * d;
+    const dim3 grid(max_q, batch, 2 * kv_heads);
+    if (dtype == LLMI_F32)
+        hipLaunchKernelGGL(kv_append_kernel<float>, grid, dim3(d), 0, s, (const float*)k_src, (const float*)v_src,
+                           (float*)k_cache + off, (float*)v_cache + off, cur_q, hist, kv_heads, d, max_q, max_seq);
+    else
+        hipLaunchKernelGGL(kv_append_kernel<__half>, grid, dim3(d), 0, s, (const __half*)k_src, (const __half*)v_src,
+                           (__half*)k_cache + off, (__half*)v_cache + off, cur_q, hist, kv_heads, d, max_q, max_seq);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int transpose_remove_pad_launch(const void* src, const int* po, void* dst, int dtype, int num_tokens, int batch,
+                                int seq_len, int heads, int d, hipStream_t s) {
+    LLMI_REQUIRE(src && po && dst && num_tokens > 0 && batch > 0 && seq_len > 0 && heads > 0 && d > 0,
+                 "transpose_remove_pad: bad arguments");
+    LLMI_REQUIRE(num_tokens <= batch * seq_len, "transpose_remove_pad: more tokens than padded positions");
+    LLMI_REQUIRE(fp_dtype(dtype), "transpose_remove_pad: dtype must be f32 or f16");
+    const int block = heads * d < 1024 ? heads * d : 1024;
+    if (dtype == LLMI_F32)
+        hipLaunchKernelGGL(transpose_remove_pad_kernel<float>, dim3(num_tokens), dim3(block), 0, s, (const float*)src,
+                           (float*)dst, po, seq_len, heads, d);
+    else
+        hipLaunchKernelGGL(transpose_remove_pad_kernel<__half>, dim3(num_tokens), dim3(block), 0, s,
+                           (const __half*)src, (__half*)dst, po, seq_len, heads, d);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+int rope_qkv_prefill_launch(const void* qkv, void* q, void* k, void* v, int dtype, const int* po, const int* hist,
+                            int num_tokens, int batch, int seq_len, int heads, int kv_heads, int d, float base,
+                            hipStream_t s) {
+    LLMI_REQUIRE(qkv && q && k && v && po && hist, "rope_qkv_prefill: null pointer");
+    LLMI_REQUIRE(num_tokens > 0 && batch > 0 && seq_len > 0 && num_tokens <= batch * seq_len,
+                 "rope_qkv_prefill: bad token counts");
+    LLMI_REQUIRE(heads > 0 && kv_heads > 0 && kv_heads <= heads && heads <= 65535 && d > 0 && d % 2 == 0 &&
+                     d <= 1024,
+                 "rope_qkv_prefill: bad head shape");
+    LLMI_REQUIRE(fp_dtype(dtype), "rope_qkv_prefill: dtype must be f32 or f16");
+    const dim3 grid(num_tokens, heads);
+    if (dtype == LLMI_F32)
+        hipLaunchKernelGGL(rope_qkv_prefill_kernel<float>, grid, dim3(d), 0, s, (const float*)qkv, (float*)q,
+                           (float*)k, (float*)v, po, hist, seq_len, heads, kv_heads, d, base);
+    else
+        hipLaunchKernelGGL(rope_qkv_prefill_kernel<__half>, grid, dim3(d), 0, s, (const __half*)qkv, (__half*)q,
+                           (__half*)k, (__half*)v, po, hist, seq_len, heads, kv_heads, d, base);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace llmi

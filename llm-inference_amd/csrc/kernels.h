@@ -284,6 +284,19 @@ int add_resid_rmsnorm_launch(float* resid, float* out, const void* bias, int b_d
                              hipStream_t s);
 int add_resid_launch(const float* resid, float* out, int n, int hidden, hipStream_t s);
 int silu_mul_launch(const float* gu, float* out, int n, int inter, hipStream_t s);
+// context-phase operators (context_ops.hip)
+int causal_mask_launch(void* mask, int dtype, const int* q_lens, const int* k_lens, int batch, int max_q, int max_k,
+                       hipStream_t s);
+int masked_softmax_launch(const void* qk, const void* mask, void* score, int dtype, int batch, int heads, int q_len,
+                          int k_len, float scale, hipStream_t s);
+int kv_append_launch(const void* k_src, const void* v_src, int dtype, int layer, const int* cur_q, const int* hist,
+                     int batch, int kv_heads, int max_q, int d, int max_seq, void* k_cache, void* v_cache,
+                     hipStream_t s);
+int transpose_remove_pad_launch(const void* src, const int* po, void* dst, int dtype, int num_tokens, int batch,
+                                int seq_len, int heads, int d, hipStream_t s);
+int rope_qkv_prefill_launch(const void* qkv, void* q, void* k, void* v, int dtype, const int* po, const int* hist,
+                            int num_tokens, int batch, int seq_len, int heads, int kv_heads, int d, float base,
+                            hipStream_t s);
 int rope_decode_launch(float* qkv, int pos, int heads, int kv_heads, int head_dim, float base,
                        hipStream_t s);
 int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long long* scratch,

@@ -47,6 +47,11 @@ _SIGS = {
     "llmi_attn_workspace_bytes": (_SZ, [_I, _I, _I]),
     "llmi_attn_decode": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P]),
     "llmi_argmax": (_I, [_P, _I, _P, _P]),
+    "llmi_rope_qkv_prefill": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
+    "llmi_kv_append": (_I, [_P, _P, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "llmi_causal_mask": (_I, [_P, _I, _P, _P, _I, _I, _I, _P]),
+    "llmi_masked_softmax": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
+    "llmi_transpose_remove_pad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_synth_fill": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I, _P]),
     "llmi_synth_fill_host": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I]),
     "llmi_synth_prompt": (_I, [_U64, _I, _I, _P]),

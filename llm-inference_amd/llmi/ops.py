@@ -122,3 +122,63 @@ def synth_fill(out: torch.Tensor, kind: int, seed: int, tid: int, rows: int, col
     _dev(out)
     call("llmi_synth_fill", out.data_ptr(), _dt(out), kind, seed, tid, rows, cols, row0, col0, ld, _stream())
     return out
+
+
+# ---------------------------------------------- context-phase (prefill) operators
+def _i32(t):
+    return t.to(torch.int32).contiguous()
+
+
+def launchAddFusedQKVBiasTransposeAndRoPE(qkv, padding_offset, history_length, batch: int, seq_len: int,
+                                          heads: int, kv_heads: int, head_dim: int = 128, base: float = 10000.0):
+    """qkv [num_tokens, (heads + 2 kv) * d] -> q [batch, heads, seq_len, d], k, v [batch, kv, seq_len, d]
+    (qkv_bias_and_RoPE.cu:49-144; no bias for Llama). Padded slots of q/k/v are zero."""
+    _dev(qkv, padding_offset, history_length)
+    n = qkv.shape[0]
+    po, hist = _i32(padding_offset), _i32(history_length)
+    q = torch.zeros(batch, heads, seq_len, head_dim, device=qkv.device, dtype=qkv.dtype)
+    k = torch.zeros(batch, kv_heads, seq_len, head_dim, device=qkv.device, dtype=qkv.dtype)
+    v = torch.zeros_like(k)
+    call("llmi_rope_qkv_prefill", qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), _dt(qkv), po.data_ptr(),
+         hist.data_ptr(), n, batch, seq_len, heads, kv_heads, head_dim, float(base), _stream())
+    return q, k, v
+
+
+def launchConcatKVCache(k_src, v_src, layer: int, cur_query_length, history_length, k_dst, v_dst):
+    """k_src/v_src [batch, kv, max_q_len, d]; k_dst/v_dst [layers, batch, kv, max_seq, d] (concat_past_kv.cu)."""
+    _dev(k_src, v_src, cur_query_length, history_length, k_dst, v_dst)
+    b, kv, max_q, d = k_src.shape
+    cq, hist = _i32(cur_query_length), _i32(history_length)
+    call("llmi_kv_append", k_src.data_ptr(), v_src.data_ptr(), _dt(k_src), int(layer), cq.data_ptr(),
+         hist.data_ptr(), b, kv, max_q, d, k_dst.shape[3], k_dst.data_ptr(), v_dst.data_ptr(), _stream())
+    return k_dst, v_dst
+
+
+def launchBuildCausalMasks(q_lens, k_lens, max_q_len: int, max_k_len: int, dtype=torch.float32):
+    _dev(q_lens, k_lens)
+    ql, kl = _i32(q_lens), _i32(k_lens)
+    mask = torch.empty(ql.numel(), max_q_len, max_k_len, device=ql.device, dtype=dtype)
+    call("llmi_causal_mask", mask.data_ptr(), _dt(mask), ql.data_ptr(), kl.data_ptr(), ql.numel(), max_q_len,
+         max_k_len, _stream())
+    return mask
+
+
+def launchScaleMaskAndSoftmax(qk, mask, scale: float, out=None):
+    """qk [batch, heads, q_len, k_len], mask [batch, q_len, k_len] -> attention scores."""
+    _dev(qk, mask)
+    b, h, ql, kl = qk.shape
+    out = torch.empty_like(qk) if out is None else out
+    call("llmi_masked_softmax", qk.data_ptr(), mask.data_ptr(), out.data_ptr(), _dt(qk), b, h, ql, kl, float(scale),
+         _stream())
+    return out
+
+
+def launchTransposeOutRemovePadding(src, padding_offset, num_tokens: int):
+    """src [batch, heads, seq_len, d] -> [num_tokens, heads * d]."""
+    _dev(src, padding_offset)
+    b, h, s, d = src.shape
+    po = _i32(padding_offset)
+    out = torch.empty(num_tokens, h * d, device=src.device, dtype=src.dtype)
+    call("llmi_transpose_remove_pad", src.data_ptr(), po.data_ptr(), out.data_ptr(), _dt(src), num_tokens, b, s, h,
+         d, _stream())
+    return out

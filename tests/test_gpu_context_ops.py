@@ -1,0 +1,167 @@
+"""Context-phase operators (context_ops.hip through the C ABI) against
+oracle/context_ops.py on the same inputs: a ragged batch with padding and history,
+fp32 and fp16 storage, and a 7B-width single sequence.
+
+Bars: bit-exact for the mask, KV append and transpose (pure moves / integer tests);
+RoPE and the softmax within the relative-L2 / absolute tolerances written below."""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import context_ops as C  # noqa: E402
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from llmi import ops as O
+    return O
+
+
+def T(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t if dtype is None else t.to(dtype)
+
+
+def N(t):
+    torch.cuda.synchronize()
+    return t.detach().float().cpu().numpy()
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+LENS, HIST = [5, 3, 7], [0, 4, 2]
+HEADS, KVH, D = 4, 2, 128
+
+
+def ragged(seed=0):
+    rng = np.random.default_rng(seed)
+    n = sum(LENS)
+    qkv = rng.standard_normal((n, (HEADS + 2 * KVH) * D)).astype(np.float32)
+    return qkv, C.padding_offset(LENS, max(LENS))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_rope_qkv_prefill_ragged(ops, dt):
+    qkv, po = ragged()
+    if dt == torch.float16:
+        qkv = qkv.astype(np.float16).astype(np.float32)
+    q, k, v = ops.launchAddFusedQKVBiasTransposeAndRoPE(T(qkv, dt), T(po), T(np.array(HIST, np.int32)), len(LENS),
+                                                        max(LENS), HEADS, KVH, D)
+    wq, wk, wv = C.rope_qkv_prefill(qkv, po, np.array(HIST), len(LENS), max(LENS), HEADS, KVH, D)
+    tol = 1e-6 if dt == torch.float32 else 1e-3  # fp16: one rounding of the stored result
+    assert rel(N(q), wq) < tol and rel(N(k), wk) < tol
+    np.testing.assert_array_equal(N(v), wv.astype(np.float16).astype(np.float32) if dt == torch.float16 else wv)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_kv_append_bit_exact(ops, dt):
+    rng = np.random.default_rng(2)
+    b, max_q, max_seq, layers, layer = len(LENS), max(LENS), 24, 3, 1
+    ks = rng.standard_normal((b, KVH, max_q, D)).astype(np.float32)
+    vs = rng.standard_normal((b, KVH, max_q, D)).astype(np.float32)
+    kc = rng.standard_normal((layers, b, KVH, max_seq, D)).astype(np.float32)
+    vc = rng.standard_normal((layers, b, KVH, max_seq, D)).astype(np.float32)
+    if dt == torch.float16:
+        ks, vs, kc, vc = (a.astype(np.float16).astype(np.float32) for a in (ks, vs, kc, vc))
+    gk, gv = T(kc, dt), T(vc, dt)
+    ops.launchConcatKVCache(T(ks, dt), T(vs, dt), layer, T(np.array(LENS, np.int32)), T(np.array(HIST, np.int32)),
+                            gk, gv)
+    wk, wv = C.kv_append(ks, vs, layer, LENS, HIST, kc.copy(), vc.copy())
+    np.testing.assert_array_equal(N(gk), wk)
+    np.testing.assert_array_equal(N(gv), wv)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_causal_mask_bit_exact(ops, dt):
+    ql, kl = np.array(LENS, np.int32), np.array([h + n for h, n in zip(HIST, LENS)], np.int32)
+    m = ops.launchBuildCausalMasks(T(ql), T(kl), int(ql.max()), int(kl.max()), dtype=dt)
+    np.testing.assert_array_equal(N(m), C.causal_mask(ql, kl, int(ql.max()), int(kl.max())))
+    one = ops.launchBuildCausalMasks(T(np.array([1], np.int32)), T(np.array([1], np.int32)), 1, 1, dtype=dt)
+    assert N(one).tolist() == [[[1.0]]]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_masked_softmax(ops, dt):
+    rng = np.random.default_rng(3)
+    ql = np.array(LENS, np.int32)
+    kl = np.array([h + n for h, n in zip(HIST, LENS)], np.int32)
+    mq, mk = int(ql.max()), int(kl.max())
+    qk = (rng.standard_normal((len(LENS), HEADS, mq, mk)) * 8).astype(np.float32)
+    mask = C.causal_mask(ql, kl, mq, mk)
+    if dt == torch.float16:
+        qk = qk.astype(np.float16).astype(np.float32)
+    got = N(ops.launchScaleMaskAndSoftmax(T(qk, dt), T(mask, dt), 1 / math.sqrt(D)))
+    want = C.masked_softmax(qk, mask, 1 / math.sqrt(D))
+    atol = 1e-6 if dt == torch.float32 else 1e-3
+    np.testing.assert_allclose(got, want, rtol=0, atol=atol)
+    # wide rows (k_len past one workgroup's 256 threads), in place
+    qk2 = (rng.standard_normal((1, 2, 3, 2500)) * 4).astype(np.float32)
+    m2 = C.causal_mask([3], [2500], 3, 2500)
+    t2 = T(qk2)
+    ops.launchScaleMaskAndSoftmax(t2, T(m2), 0.25, out=t2)
+    np.testing.assert_allclose(N(t2), C.masked_softmax(qk2, m2, 0.25), rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_transpose_remove_pad_bit_exact(ops, dt):
+    rng = np.random.default_rng(4)
+    src = rng.standard_normal((len(LENS), HEADS, max(LENS), D)).astype(np.float32)
+    if dt == torch.float16:
+        src = src.astype(np.float16).astype(np.float32)
+    po = C.padding_offset(LENS, max(LENS))
+    got = ops.launchTransposeOutRemovePadding(T(src, dt), T(po), sum(LENS))
+    np.testing.assert_array_equal(N(got), C.transpose_remove_pad(src, po, sum(LENS)))
+
+
+def chain(ops, qkv, lens, hist, heads, kvh, max_seq):
+    """The reference's context attention from the llmi operators; QK^T and PV (its
+    launchLinearStridedBatchGemm) by torch.matmul -- test plumbing only."""
+    b, mq = len(lens), max(lens)
+    po = C.padding_offset(lens, mq)
+    q, k, v = ops.launchAddFusedQKVBiasTransposeAndRoPE(T(qkv), T(po), T(np.array(hist, np.int32)), b, mq, heads,
+                                                        kvh, D)
+    kc = torch.zeros(1, b, kvh, max_seq, D, device=DEV)
+    vc = torch.zeros_like(kc)
+    ops.launchConcatKVCache(k, v, 0, T(np.array(lens, np.int32)), T(np.array(hist, np.int32)), kc, vc)
+    kl = [h + n for h, n in zip(hist, lens)]
+    mk = max(kl)
+    g = heads // kvh
+    kk = kc[0, :, :, :mk].repeat_interleave(g, dim=1)
+    vv = vc[0, :, :, :mk].repeat_interleave(g, dim=1)
+    qk = torch.matmul(q, kk.transpose(-1, -2))
+    mask = ops.launchBuildCausalMasks(T(np.array(lens, np.int32)), T(np.array(kl, np.int32)), mq, mk)
+    p = ops.launchScaleMaskAndSoftmax(qk, mask, 1 / math.sqrt(D))
+    o = torch.matmul(p, vv)
+    return N(ops.launchTransposeOutRemovePadding(o.contiguous(), T(po), sum(lens)))
+
+
+def test_context_attention_chain_ragged(ops):
+    torch.backends.cuda.matmul.allow_tf32 = False
+    qkv, _ = ragged(5)
+    got = chain(ops, qkv, LENS, HIST, HEADS, KVH, 16)
+    want = C.context_attention(qkv, LENS, HIST, HEADS, KVH, D, np.zeros((1, 3, KVH, 16, D), np.float32),
+                               np.zeros((1, 3, KVH, 16, D), np.float32))
+    assert rel(got, want) < 1e-5
+
+
+def test_context_attention_chain_7b_width():
+    """Llama-2-7B heads (32 x 128), one 512-token sequence, no history (config 3 shape)."""
+    from llmi import ops
+    torch.backends.cuda.matmul.allow_tf32 = False
+    rng = np.random.default_rng(6)
+    n, h = 512, 32
+    qkv = rng.standard_normal((n, 3 * h * D)).astype(np.float32)
+    got = chain(ops, qkv, [n], [0], h, h, n)
+    want = C.context_attention(qkv, [n], [0], h, h, D, np.zeros((1, 1, h, n, D), np.float32),
+                               np.zeros((1, 1, h, n, D), np.float32))
+    assert rel(got, want) < 1e-5
