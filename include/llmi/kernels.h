@@ -139,3 +139,69 @@ inline void launchTopKforBeamSearch(TensorWrapper<float>* probs, TensorWrapper<i
                                     void* stream = nullptr) {
     LLMI_CALL(llmi_argmax(probs->data, probs->shape.back(), final_topk_id->data, stream));
 }
+
+// ---- context-phase launchers (prefill; the engine fuses them, see llmi_engine_prefill).
+// T = float or half_t storage; padding_offset, history_length, input_length, q_lens,
+// k_lens, cur_query_length are device int tensors; layer_id is a host tensor.
+
+// qkv_bias_and_RoPE.h:26-36 -- QKV [num_tokens, heads + 2 kv_heads, head] ->
+// q [batch, heads, seq, head], k, v [batch, kv_heads, seq, head], RoPE at history + s.
+// Llama has no qkv bias (qkv.bias is ignored); v is written (the reference leaves it
+// unset) and positions are per sequence (include/llmi.h: llmi_rope_qkv_prefill).
+template <typename T>
+void launchAddFusedQKVBiasTransposeAndRoPE(TensorWrapper<T>* q_buf, TensorWrapper<T>* k_buf, TensorWrapper<T>* v_buf,
+                                           TensorWrapper<T>* QKV, BaseWeight<T>& qkv,
+                                           TensorWrapper<int>* padding_offset, TensorWrapper<int>* history_length,
+                                           TensorWrapper<int>* input_length, LLaMAAttentionStaticParams& params,
+                                           void* stream = nullptr) {
+    (void)qkv;
+    (void)input_length;
+    LLM_CHECK_WITH_INFO(q_buf->shape.size() == 4 && k_buf->shape.size() == 4, "q/k/v bufs must be [bs, heads, seq, head]");
+    const int batch = q_buf->shape[0], heads = q_buf->shape[1], seq = q_buf->shape[2], head = q_buf->shape[3];
+    const int kv = k_buf->shape[1];
+    const int tokens = QKV->size() / ((heads + 2 * kv) * head);
+    LLMI_CALL(llmi_rope_qkv_prefill(QKV->data, q_buf->data, k_buf->data, v_buf->data, llmiDtype(getTensorType<T>()),
+                                    padding_offset->data, history_length->data, tokens, batch, seq, heads, kv, head,
+                                    params.rotary_embedding_base, stream));
+}
+
+// concat_past_kv.h:11-18 -- k/v [bs, kv_heads, max_q_len, head] -> caches
+// [layers, bs, kv_heads, max_seq, head] at slots history_length[b] + t, t < cur_query_length[b].
+template <typename T>
+void launchConcatKVCache(TensorWrapper<T>* k_src, TensorWrapper<T>* v_src, TensorWrapper<int>* layer_id,
+                         TensorWrapper<int>* cur_query_length, TensorWrapper<int>* history_length,
+                         TensorWrapper<T>* k_dst, TensorWrapper<T>* v_dst, void* stream = nullptr) {
+    LLM_CHECK_WITH_INFO(k_src->shape.size() == 4 && k_dst->shape.size() == 5, "concat kv: bad shapes");
+    LLMI_CALL(llmi_kv_append(k_src->data, v_src->data, llmiDtype(getTensorType<T>()), layer_id->getVal(),
+                             cur_query_length->data, history_length->data, k_src->shape[0], k_src->shape[1],
+                             k_src->shape[2], k_src->shape[3], k_dst->shape[3], k_dst->data, v_dst->data, stream));
+}
+
+// build_causal_mask.h:8-11 -- mask [bs, max_q_len, max_k_len]
+template <typename T>
+void launchBuildCausalMasks(TensorWrapper<T>* mask, TensorWrapper<int>* q_lens, TensorWrapper<int>* k_lens,
+                            void* stream = nullptr) {
+    LLM_CHECK_WITH_INFO(mask->shape.size() == 3, "mask must be [bs, max_q_len, max_k_len]");
+    LLMI_CALL(llmi_causal_mask(mask->data, llmiDtype(getTensorType<T>()), q_lens->data, k_lens->data, mask->shape[0],
+                               mask->shape[1], mask->shape[2], stream));
+}
+
+// attn_softmax_kernel.h:8-12 -- qk, attn_score [bs, heads, q_len, k_len], mask [bs, q_len, k_len]
+template <typename T>
+void launchScaleMaskAndSoftmax(TensorWrapper<T>* qk, TensorWrapper<T>* mask, TensorWrapper<T>* attn_score, float scale,
+                               void* stream = nullptr) {
+    LLM_CHECK_WITH_INFO(qk->shape.size() == 4 && mask->shape.size() == 3, "softmax: bad shapes");
+    LLMI_CALL(llmi_masked_softmax(qk->data, mask->data, attn_score->data, llmiDtype(getTensorType<T>()), qk->shape[0],
+                                  qk->shape[1], qk->shape[2], qk->shape[3], scale, stream));
+}
+
+// fused_transpose_and_remv_pad.h:7-9 -- [bs, heads, seq, head] -> [num_tokens, heads, head]
+template <typename T>
+void launchTransposeOutRemovePadding(TensorWrapper<T>* qkv_buf_w_pad, TensorWrapper<int>* padding_offset,
+                                     TensorWrapper<T>* qkv_buf_wo_pad_1, void* stream = nullptr) {
+    const int batch = qkv_buf_w_pad->shape[0], heads = qkv_buf_w_pad->shape[1];
+    const int seq = qkv_buf_w_pad->shape[2], head = qkv_buf_w_pad->shape[3];
+    LLMI_CALL(llmi_transpose_remove_pad(qkv_buf_w_pad->data, padding_offset->data, qkv_buf_wo_pad_1->data,
+                                        llmiDtype(getTensorType<T>()), qkv_buf_wo_pad_1->shape[0], batch, seq, heads,
+                                        head, stream));
+}
