@@ -147,6 +147,13 @@ int llmi_causal_mask(void* mask, int dtype, const int32_t* q_lens, const int32_t
 int llmi_masked_softmax(const void* qk, const void* mask, void* score, int dtype, int batch, int heads, int q_len,
                         int k_len, float scale, llmi_stream_t stream);
 
+/* launchLinearStridedBatchGemm (src/kernels/linear.h:29-36, .cu:126-229): for each of
+ * `batch` matrices (contiguous, row-major) c[z] = op(a[z]) . op(b[z]); op(a) [m, k] is a
+ * [m, k] or, with trans_a, a [k, m]; op(b) [k, n] is b [k, n] or, with trans_b, b [n, k];
+ * c [m, n]; fp32 accumulate. QK^T: a = q, b = k, trans_b = 1; PV: a = scores, b = v. */
+int llmi_batched_matmul(const void* a, const void* b, void* c, int dtype, int batch, int m, int n, int k, int trans_a,
+                        int trans_b, llmi_stream_t stream);
+
 /* launchTransposeOutRemovePadding (src/kernels/fused_transpose_and_remv_pad.h:7-9,
  * .cu:17-75): src [batch, heads, seq_len, d] -> dst [num_tokens, heads * d], token i
  * read from padded position i + padding_offset[i]. */

@@ -205,3 +205,22 @@ void launchTransposeOutRemovePadding(TensorWrapper<T>* qkv_buf_w_pad, TensorWrap
                                         llmiDtype(getTensorType<T>()), qkv_buf_wo_pad_1->shape[0], batch, seq, heads,
                                         head, stream));
 }
+
+// linear.h:29-36 -- output[b, h] = op(input1[b, h]) . op(input2[b, h]) (QK^T: input1 = q,
+// input2 = k, trans_b = true; PV: input1 = scores, input2 = v). The intended semantics of
+// linear.cu:126-229 (its strideC = Cm * Cm is only right for square outputs); heads of
+// input2 must equal input1's (expand GQA k/v first, as the reference's repeat_kv).
+template <typename T>
+void launchLinearStridedBatchGemm(TensorWrapper<T>* input1, TensorWrapper<T>* input2, TensorWrapper<T>* output,
+                                  cublasWrapper* cublas_wrapper = nullptr, bool trans_a = false, bool trans_b = false) {
+    LLM_CHECK_WITH_INFO(input1->shape.size() == 4 && input2->shape.size() == 4 && output->shape.size() == 4,
+                        "strided batch gemm: tensors must be [bs, heads, rows, cols]");
+    const int batch = input1->shape[0] * input1->shape[1];
+    const int m = trans_a ? input1->shape[3] : input1->shape[2], k = trans_a ? input1->shape[2] : input1->shape[3];
+    const int k2 = trans_b ? input2->shape[3] : input2->shape[2], n = trans_b ? input2->shape[2] : input2->shape[3];
+    LLM_CHECK_WITH_INFO(k == k2, "2nd dim of input MUST = 1st dim of weight");
+    LLM_CHECK_WITH_INFO(input2->shape[0] * input2->shape[1] == batch, "strided batch gemm: batch counts differ");
+    LLM_CHECK_WITH_INFO(output->shape[2] == m && output->shape[3] == n, "strided batch gemm: bad output shape");
+    LLMI_CALL(llmi_batched_matmul(input1->data, input2->data, output->data, llmiDtype(getTensorType<T>()), batch, m, n,
+                                  k, trans_a ? 1 : 0, trans_b ? 1 : 0, cublas_wrapper ? cublas_wrapper->stream : nullptr));
+}

@@ -128,6 +128,11 @@ int llmi_masked_softmax(const void* qk, const void* mask, void* score, int dtype
     return masked_softmax_launch(qk, mask, score, dtype, batch, heads, q_len, k_len, scale, STREAM(stream));
 }
 
+int llmi_batched_matmul(const void* a, const void* b, void* c, int dtype, int batch, int m, int n, int k, int trans_a,
+                        int trans_b, llmi_stream_t stream) {
+    return batched_matmul_launch(a, b, c, dtype, batch, m, n, k, trans_a, trans_b, STREAM(stream));
+}
+
 int llmi_transpose_remove_pad(const void* src, const int32_t* padding_offset, void* dst, int dtype, int num_tokens,
                               int batch, int seq_len, int heads, int head_dim, llmi_stream_t stream) {
     return transpose_remove_pad_launch(src, padding_offset, dst, dtype, num_tokens, batch, seq_len, heads, head_dim,

@@ -231,3 +231,93 @@ int rope_qkv_prefill_launch(const void* qkv, void* q, void* k, void* v, int dtyp
 }
 
 }  // namespace llmi
+
+// ------------------------------------------------ strided batched matmul
+namespace llmi {
+namespace {
+// launchLinearStridedBatchGemm (linear.cu:126-229: cublas stridedBatchedGemm for QK^T
+// and PV of the unfused context attention): C[z] = op(A[z]) . op(B[z]), row-major,
+// A [m, k] (or [k, m] when trans_a), B [k, n] (or [n, k] when trans_b), fp32
+// accumulate. 64 x 64 output tile per 256-thread workgroup, 4 x 4 per thread, K in
+// 16-deep LDS slabs (padded rows: conflict-free). The engine's prefill does these
+// products on the matrix cores inside its fused attention (prefill.hip); this is the
+// operator-level form for callers of the unfused layer.
+constexpr int kBT = 64, kKT = 16;
+template <typename T, bool TA, bool TB>
+__global__ __launch_bounds__(256) void bmm_kernel(const T* A, const T* B, T* C, int m, int n, int k) {
+    __shared__ float As[kKT][kBT + 4];
+    __shared__ float Bs[kKT][kBT + 4];
+    const size_t z = blockIdx.z;
+    A += z * m * (size_t)k;
+    B += z * k * (size_t)n;
+    C += z * m * (size_t)n;
+    const int r0 = blockIdx.y * kBT, c0 = blockIdx.x * kBT;
+    const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+    float acc[4][4] = {};
+    for (int k0 = 0; k0 < k; k0 += kKT) {
+        for (int e = threadIdx.x; e < kBT * kKT; e += 256) {
+            const int rr = TA ? e % kBT : e / kKT, kk = TA ? e / kBT : e % kKT;  // coalesced along memory
+            const int r = r0 + rr, kx = k0 + kk;
+            As[kk][rr] = (r < m && kx < k) ? ldf(TA ? A + (size_t)kx * m + r : A + (size_t)r * k + kx) : 0.f;
+        }
+        for (int e = threadIdx.x; e < kBT * kKT; e += 256) {
+            const int cc = TB ? e / kKT : e % kBT, kk = TB ? e % kKT : e / kBT;
+            const int c = c0 + cc, kx = k0 + kk;
+            Bs[kk][cc] = (c < n && kx < k) ? ldf(TB ? B + (size_t)c * k + kx : B + (size_t)kx * n + c) : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < kKT; ++kk) {
+            float a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = r0 + ty * 4 + i;
+        if (r >= m) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = c0 + tx * 4 + j;
+            if (c < n) stf(C + (size_t)r * n + c, acc[i][j]);
+        }
+    }
+}
+
+template <typename T>
+void bmm_dispatch(const void* a, const void* b, void* c, int batch, int m, int n, int k, bool ta, bool tb,
+                  hipStream_t s) {
+    const dim3 grid((n + kBT - 1) / kBT, (m + kBT - 1) / kBT, batch);
+    const T* A = (const T*)a;
+    const T* B = (const T*)b;
+    T* C = (T*)c;
+    if (!ta && !tb) hipLaunchKernelGGL((bmm_kernel<T, false, false>), grid, dim3(256), 0, s, A, B, C, m, n, k);
+    if (!ta && tb) hipLaunchKernelGGL((bmm_kernel<T, false, true>), grid, dim3(256), 0, s, A, B, C, m, n, k);
+    if (ta && !tb) hipLaunchKernelGGL((bmm_kernel<T, true, false>), grid, dim3(256), 0, s, A, B, C, m, n, k);
+    if (ta && tb) hipLaunchKernelGGL((bmm_kernel<T, true, true>), grid, dim3(256), 0, s, A, B, C, m, n, k);
+}
+}  // namespace
+
+int batched_matmul_launch(const void* a, const void* b, void* c, int dtype, int batch, int m, int n, int k,
+                          int trans_a, int trans_b, hipStream_t s) {
+    LLMI_REQUIRE(a && b && c, "batched_matmul: null pointer");
+    LLMI_REQUIRE(batch > 0 && batch <= 65535 && m > 0 && n > 0 && k > 0, "batched_matmul: bad shape");
+    LLMI_REQUIRE(m <= 65535 * kBT, "batched_matmul: m too large");
+    LLMI_REQUIRE(fp_dtype(dtype), "batched_matmul: dtype must be f32 or f16");
+    if (dtype == LLMI_F32)
+        bmm_dispatch<float>(a, b, c, batch, m, n, k, trans_a != 0, trans_b != 0, s);
+    else
+        bmm_dispatch<__half>(a, b, c, batch, m, n, k, trans_a != 0, trans_b != 0, s);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace llmi

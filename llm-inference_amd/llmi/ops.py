@@ -182,3 +182,19 @@ def launchTransposeOutRemovePadding(src, padding_offset, num_tokens: int):
     call("llmi_transpose_remove_pad", src.data_ptr(), po.data_ptr(), out.data_ptr(), _dt(src), num_tokens, b, s, h,
          d, _stream())
     return out
+
+
+def launchLinearStridedBatchGemm(input1, input2, trans_a: bool = False, trans_b: bool = False):
+    """input1 [bs, heads, m|k, k|m], input2 [bs, heads, k|n, n|k] -> [bs, heads, m, n] =
+    op(input1) @ op(input2) (linear.cu:126-229; QK^T with trans_b, PV without)."""
+    _dev(input1, input2)
+    b, h = input1.shape[0], input1.shape[1]
+    m, k = (input1.shape[3], input1.shape[2]) if trans_a else (input1.shape[2], input1.shape[3])
+    k2, n = (input2.shape[3], input2.shape[2]) if trans_b else (input2.shape[2], input2.shape[3])
+    if k != k2 or input2.shape[0] * input2.shape[1] != b * h:
+        raise ValueError("launchLinearStridedBatchGemm: inner dims / batch counts differ")
+    a, bb = input1.contiguous(), input2.contiguous()
+    out = torch.empty(b, h, m, n, device=input1.device, dtype=input1.dtype)
+    call("llmi_batched_matmul", a.data_ptr(), bb.data_ptr(), out.data_ptr(), _dt(a), b * h, m, n, k,
+         1 if trans_a else 0, 1 if trans_b else 0, _stream())
+    return out

@@ -124,8 +124,8 @@ def test_transpose_remove_pad_bit_exact(ops, dt):
 
 
 def chain(ops, qkv, lens, hist, heads, kvh, max_seq):
-    """The reference's context attention from the llmi operators; QK^T and PV (its
-    launchLinearStridedBatchGemm) by torch.matmul -- test plumbing only."""
+    """The reference's context attention, every step an llmi operator (the GQA head
+    expansion, the reference's repeat_kv, is torch plumbing here)."""
     b, mq = len(lens), max(lens)
     po = C.padding_offset(lens, mq)
     q, k, v = ops.launchAddFusedQKVBiasTransposeAndRoPE(T(qkv), T(po), T(np.array(hist, np.int32)), b, mq, heads,
@@ -138,15 +138,14 @@ def chain(ops, qkv, lens, hist, heads, kvh, max_seq):
     g = heads // kvh
     kk = kc[0, :, :, :mk].repeat_interleave(g, dim=1)
     vv = vc[0, :, :, :mk].repeat_interleave(g, dim=1)
-    qk = torch.matmul(q, kk.transpose(-1, -2))
+    qk = ops.launchLinearStridedBatchGemm(q, kk, trans_b=True)
     mask = ops.launchBuildCausalMasks(T(np.array(lens, np.int32)), T(np.array(kl, np.int32)), mq, mk)
     p = ops.launchScaleMaskAndSoftmax(qk, mask, 1 / math.sqrt(D))
-    o = torch.matmul(p, vv)
+    o = ops.launchLinearStridedBatchGemm(p, vv)
     return N(ops.launchTransposeOutRemovePadding(o.contiguous(), T(po), sum(lens)))
 
 
 def test_context_attention_chain_ragged(ops):
-    torch.backends.cuda.matmul.allow_tf32 = False
     qkv, _ = ragged(5)
     got = chain(ops, qkv, LENS, HIST, HEADS, KVH, 16)
     want = C.context_attention(qkv, LENS, HIST, HEADS, KVH, D, np.zeros((1, 3, KVH, 16, D), np.float32),
@@ -157,7 +156,6 @@ def test_context_attention_chain_ragged(ops):
 def test_context_attention_chain_7b_width():
     """Llama-2-7B heads (32 x 128), one 512-token sequence, no history (config 3 shape)."""
     from llmi import ops
-    torch.backends.cuda.matmul.allow_tf32 = False
     rng = np.random.default_rng(6)
     n, h = 512, 32
     qkv = rng.standard_normal((n, 3 * h * D)).astype(np.float32)
@@ -165,3 +163,21 @@ def test_context_attention_chain_7b_width():
     want = C.context_attention(qkv, [n], [0], h, h, D, np.zeros((1, 1, h, n, D), np.float32),
                                np.zeros((1, 1, h, n, D), np.float32))
     assert rel(got, want) < 1e-5
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_strided_batch_gemm(ops, ta, tb, dt):
+    """Ragged tile edges (m, n, k not multiples of 64 / 16), 2 x 3 batch."""
+    rng = np.random.default_rng(8)
+    m, n, k = 70, 45, 37
+    a = rng.standard_normal((2, 3, k, m) if ta else (2, 3, m, k)).astype(np.float32)
+    b = rng.standard_normal((2, 3, n, k) if tb else (2, 3, k, n)).astype(np.float32)
+    if dt == torch.float16:
+        a, b = a.astype(np.float16).astype(np.float32), b.astype(np.float16).astype(np.float32)
+    got = N(ops.launchLinearStridedBatchGemm(T(a, dt), T(b, dt), trans_a=ta, trans_b=tb))
+    oa = np.swapaxes(a, -1, -2) if ta else a
+    ob = np.swapaxes(b, -1, -2) if tb else b
+    want = np.matmul(oa.astype(np.float64), ob.astype(np.float64))
+    assert got.shape == (2, 3, m, n)
+    assert rel(got, want) < (1e-6 if dt == torch.float32 else 1e-3)
