@@ -34,7 +34,7 @@ extern "C" {
 
 typedef void* llmi_stream_t; /* hipStream_t; NULL = legacy default stream */
 
-enum llmi_dtype { LLMI_F32 = 0, LLMI_F16 = 1, LLMI_I8 = 2, LLMI_I32 = 3 };
+enum llmi_dtype { LLMI_F32 = 0, LLMI_F16 = 1, LLMI_I8 = 2, LLMI_I32 = 3, LLMI_I64 = 4 };
 
 #define LLMI_OK 0
 #define LLMI_EINVAL (-1)
@@ -209,6 +209,18 @@ int llmi_config_preset(const char* name, llmi_config* cfg);
 /* RCCL unique id (128 bytes) for tensor parallel: rank 0 creates it, the
  * launcher broadcasts it (any side channel), every rank passes it to create. */
 int llmi_tp_unique_id(void* out128);
+
+/* Tensor-parallel all-reduce for operator-level callers (the sum of the
+ * row-parallel partials after o_proj and down, modeling_llama.py pretraining_tp
+ * semantics; the reference has none). One communicator per rank over RCCL (xGMI):
+ * llmi_tp_comm_create on `device` with the broadcast id; llmi_tp_allreduce sums `count`
+ * elements of buf in place across the ranks on `stream` (dtype LLMI_F32, LLMI_F16,
+ * LLMI_I32 or LLMI_I64 -- the engine reduces its int64 fixed-point residual, exact and
+ * order-independent). The engine owns its own communicator (llmi_engine_create). */
+typedef struct llmi_tp_comm llmi_tp_comm;
+int llmi_tp_comm_create(const void* tp_id, int world, int rank, int device, llmi_tp_comm** out);
+int llmi_tp_allreduce(llmi_tp_comm* comm, void* buf, size_t count, int dtype, llmi_stream_t stream);
+int llmi_tp_comm_destroy(llmi_tp_comm* comm);
 
 /* device: HIP device ordinal. tp_id: 128-byte RCCL id or NULL when tp_world == 1. */
 int llmi_engine_create(const llmi_config* cfg, int device, const void* tp_id, llmi_engine** out);

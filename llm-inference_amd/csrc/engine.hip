@@ -891,6 +891,10 @@ struct Group {
 
 // ============================================================== C ABI (engine)
 using llmi::Engine;
+struct llmi_tp_comm {
+    ncclComm_t c = nullptr;
+};
+
 struct llmi_engine {
     Engine e;
 };
@@ -934,6 +938,43 @@ int llmi_tp_unique_id(void* out128) {
     LLMI_REQUIRE(r == ncclSuccess, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
     static_assert(sizeof(id) == 128, "ncclUniqueId must be 128 bytes");
     std::memcpy(out128, &id, sizeof(id));
+    return LLMI_OK;
+}
+
+int llmi_tp_comm_create(const void* tp_id, int world, int rank, int device, llmi_tp_comm** out) {
+    LLMI_REQUIRE(tp_id && out && world >= 1 && rank >= 0 && rank < world, "tp_comm_create: bad arguments");
+    *out = nullptr;
+    LLMI_HIP(hipSetDevice(device));
+    ncclUniqueId id;
+    std::memcpy(&id, tp_id, sizeof(id));
+    auto h = std::make_unique<llmi_tp_comm>();
+    ncclResult_t r = ncclCommInitRank(&h->c, world, id, rank);
+    LLMI_REQUIRE(r == ncclSuccess, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    *out = h.release();
+    return LLMI_OK;
+}
+
+int llmi_tp_allreduce(llmi_tp_comm* comm, void* buf, size_t count, int dtype, llmi_stream_t stream) {
+    LLMI_REQUIRE(comm && comm->c && (buf || count == 0), "tp_allreduce: bad arguments");
+    ncclDataType_t t;
+    switch (dtype) {
+        case LLMI_F32: t = ncclFloat32; break;
+        case LLMI_F16: t = ncclFloat16; break;
+        case LLMI_I32: t = ncclInt32; break;
+        case LLMI_I64: t = ncclInt64; break;
+        default: LLMI_REQUIRE(false, "tp_allreduce: dtype must be f32, f16, i32 or i64");
+    }
+    if (count == 0) return LLMI_OK;
+    ncclResult_t r = ncclAllReduce(buf, buf, count, t, ncclSum, comm->c, reinterpret_cast<hipStream_t>(stream));
+    LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return LLMI_OK;
+}
+
+int llmi_tp_comm_destroy(llmi_tp_comm* comm) {
+    if (!comm) return LLMI_OK;
+    ncclResult_t r = comm->c ? ncclCommDestroy(comm->c) : ncclSuccess;
+    delete comm;
+    LLMI_REQUIRE(r == ncclSuccess, std::string("ncclCommDestroy: ") + ncclGetErrorString(r));
     return LLMI_OK;
 }
 

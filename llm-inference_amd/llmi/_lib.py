@@ -15,7 +15,7 @@ REPO = os.path.dirname(PKG)
 LIB_PATH = os.environ.get("LLMI_LIB_PATH") or os.path.join(PKG, "lib", "libllmi.so")
 HEADER = os.path.join(REPO, "include", "llmi.h")
 
-F32, F16, I8, I32 = 0, 1, 2, 3
+F32, F16, I8, I32, I64 = 0, 1, 2, 3, 4
 SYN_LINEAR, SYN_EMBED, SYN_GAMMA, SYN_INT8, SYN_INT8_SCALE = 0, 1, 2, 3, 4
 
 
@@ -62,6 +62,9 @@ _SIGS = {
     "llmi_device_sync": (_I, []),
     "llmi_config_preset": (_I, [C.c_char_p, C.POINTER(Config)]),
     "llmi_tp_unique_id": (_I, [_P]),
+    "llmi_tp_comm_create": (_I, [_P, _I, _I, _I, C.POINTER(_P)]),
+    "llmi_tp_allreduce": (_I, [_P, _P, _SZ, _I, _P]),
+    "llmi_tp_comm_destroy": (_I, [_P]),
     "llmi_engine_create": (_I, [C.POINTER(Config), _I, _P, C.POINTER(_P)]),
     "llmi_engine_destroy": (_I, [_P]),
     "llmi_engine_load_synthetic": (_I, [_P, _U64]),

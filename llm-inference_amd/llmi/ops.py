@@ -10,9 +10,9 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from ._lib import F16, F32, I8, call
+from ._lib import F16, F32, I8, I32, I64, call
 
-_DT = {torch.float32: F32, torch.float16: F16, torch.int8: I8}
+_DT = {torch.float32: F32, torch.float16: F16, torch.int8: I8, torch.int32: I32, torch.int64: I64}
 
 
 def _stream():
@@ -198,3 +198,40 @@ def launchLinearStridedBatchGemm(input1, input2, trans_a: bool = False, trans_b:
     call("llmi_batched_matmul", a.data_ptr(), bb.data_ptr(), out.data_ptr(), _dt(a), b * h, m, n, k,
          1 if trans_a else 0, 1 if trans_b else 0, _stream())
     return out
+
+
+# ------------------------------------------------------ tensor-parallel all-reduce
+def tp_unique_id() -> bytes:
+    import ctypes as C
+    buf = C.create_string_buffer(128)
+    call("llmi_tp_unique_id", C.cast(buf, C.c_void_p))
+    return buf.raw
+
+
+class TPComm:
+    """One rank's RCCL communicator (llmi_tp_comm_*): all_reduce sums a device tensor in
+    place across the ranks -- the TP reduction of row-parallel partials."""
+
+    def __init__(self, unique_id: bytes, world: int, rank: int, device: int = 0):
+        import ctypes as C
+        self._h = C.c_void_p()
+        idb = C.create_string_buffer(unique_id, 128)
+        call("llmi_tp_comm_create", C.cast(idb, C.c_void_p), world, rank, device, C.byref(self._h))
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        _dev(t)
+        if not t.is_contiguous():
+            raise ValueError("all_reduce needs a contiguous tensor")
+        call("llmi_tp_allreduce", self._h, t.data_ptr(), t.numel(), _dt(t), _stream())
+        return t
+
+    def close(self):
+        if self._h:
+            call("llmi_tp_comm_destroy", self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

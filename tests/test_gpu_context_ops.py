@@ -181,3 +181,16 @@ def test_strided_batch_gemm(ops, ta, tb, dt):
     want = np.matmul(oa.astype(np.float64), ob.astype(np.float64))
     assert got.shape == (2, 3, m, n)
     assert rel(got, want) < (1e-6 if dt == torch.float32 else 1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.int32, torch.int64])
+def test_tp_allreduce_single_rank(ops, dt):
+    """llmi_tp_comm_create / llmi_tp_allreduce / llmi_tp_comm_destroy over RCCL with one
+    rank (this box has one GPU): the sum over one rank is the input, bit for bit; the
+    multi-rank reduction is exercised by bench.py --gpus N through the engine."""
+    x = (torch.arange(4099, device=DEV) % 97 - 48).to(dt)
+    ref = x.clone()
+    with ops.TPComm(ops.tp_unique_id(), 1, 0, torch.cuda.current_device()) as comm:
+        comm.all_reduce(x)
+        torch.cuda.synchronize()
+    assert torch.equal(x, ref)
