@@ -114,6 +114,13 @@ int llmi_argmax(const float* logits, int n, int32_t* out_id, llmi_stream_t strea
  * LLMI_F32 or LLMI_F16 for every tensor of a call (fp32 arithmetic); integer arrays
  * are device int32. Layouts are the reference's. */
 
+/* launchCalPaddingoffset (src/kernels/cal_paddingoffset.h, .cu:51-86): input_lengths
+ * [batch] -> padding_offset [sum of lengths] (token i sits at padded position
+ * i + padding_offset[i] of [batch, max_q_len]) and cum_seqlens [batch + 1]. Lengths must
+ * be <= max_q_len (the reference does not check; not checked on the device either). */
+int llmi_padding_offset(int32_t* padding_offset, int32_t* cum_seqlens, const int32_t* input_lengths, int batch,
+                        int max_q_len, llmi_stream_t stream);
+
 /* launchAddFusedQKVBiasTransposeAndRoPE (src/kernels/qkv_bias_and_RoPE.h:26-36,
  * .cu:49-144), Llama (no bias): qkv [num_tokens, (heads + 2 kv_heads) * d] ->
  * q [batch, heads, seq_len, d], k, v [batch, kv_heads, seq_len, d]; token i goes to

@@ -224,3 +224,15 @@ void launchLinearStridedBatchGemm(TensorWrapper<T>* input1, TensorWrapper<T>* in
     LLMI_CALL(llmi_batched_matmul(input1->data, input2->data, output->data, llmiDtype(getTensorType<T>()), batch, m, n,
                                   k, trans_a ? 1 : 0, trans_b ? 1 : 0, cublas_wrapper ? cublas_wrapper->stream : nullptr));
 }
+
+// cal_paddingoffset.h -- padding_offset [batch, max_q_len] (its first num_tokens entries
+// are written), cum_seqlens [batch + 1], input_lengths [batch] (all device int)
+inline void launchCalPaddingoffset(TensorWrapper<int>* padding_offset, TensorWrapper<int>* cum_seqlens,
+                                   TensorWrapper<int>* input_lengths, void* stream = nullptr) {
+    const int batch = padding_offset->shape[0], max_q_len = padding_offset->shape[1];
+    LLM_CHECK_WITH_INFO(batch == input_lengths->shape[0], "input lengths numbers should equal to padding offset bs dim");
+    LLM_CHECK_WITH_INFO(batch == cum_seqlens->shape[0] - 1,
+                        "cum seqlen numbers should equal to padding offset bs dim + 1!");
+    LLMI_CALL(llmi_padding_offset(padding_offset->data, cum_seqlens->data, input_lengths->data, batch, max_q_len,
+                                  stream));
+}

@@ -104,6 +104,11 @@ int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_d
     return attn_decode_launch(a, STREAM(stream));
 }
 
+int llmi_padding_offset(int32_t* padding_offset, int32_t* cum_seqlens, const int32_t* input_lengths, int batch,
+                        int max_q_len, llmi_stream_t stream) {
+    return padding_offset_launch(padding_offset, cum_seqlens, input_lengths, batch, max_q_len, STREAM(stream));
+}
+
 int llmi_rope_qkv_prefill(const void* qkv, void* q, void* k, void* v, int dtype, const int32_t* padding_offset,
                           const int32_t* history_length, int num_tokens, int batch, int seq_len, int heads,
                           int kv_heads, int head_dim, float rope_base, llmi_stream_t stream) {

@@ -321,3 +321,29 @@ int batched_matmul_launch(const void* a, const void* b, void* c, int dtype, int 
 }
 
 }  // namespace llmi
+
+// ------------------------------------------------ padding offsets
+namespace llmi {
+namespace {
+// CalPaddingoffset (cal_paddingoffset.cu:51-72): one workgroup; thread b sums the
+// lengths before sequence b (batch is small) and writes its tokens' offsets.
+__global__ void padding_offset_kernel(int* po, int* cum, const int* lens, int batch, int max_q) {
+    for (int b = threadIdx.x; b < batch; b += blockDim.x) {
+        int before = 0;
+        for (int j = 0; j < b; ++j) before += lens[j];
+        const int off = b * max_q - before;
+        for (int i = 0; i < lens[b]; ++i) po[before + i] = off;
+        cum[b] = before;
+        if (b == batch - 1) cum[batch] = before + lens[b];
+    }
+}
+}  // namespace
+
+int padding_offset_launch(int* po, int* cum, const int* lens, int batch, int max_q, hipStream_t s) {
+    LLMI_REQUIRE(po && cum && lens && batch > 0 && max_q > 0, "padding_offset: bad arguments");
+    hipLaunchKernelGGL(padding_offset_kernel, dim3(1), dim3(256), 0, s, po, cum, lens, batch, max_q);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace llmi

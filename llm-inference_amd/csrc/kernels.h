@@ -296,6 +296,7 @@ int transpose_remove_pad_launch(const void* src, const int* po, void* dst, int d
                                 int seq_len, int heads, int d, hipStream_t s);
 int batched_matmul_launch(const void* a, const void* b, void* c, int dtype, int batch, int m, int n, int k,
                           int trans_a, int trans_b, hipStream_t s);
+int padding_offset_launch(int* po, int* cum, const int* lens, int batch, int max_q, hipStream_t s);
 int rope_qkv_prefill_launch(const void* qkv, void* q, void* k, void* v, int dtype, const int* po, const int* hist,
                             int num_tokens, int batch, int seq_len, int heads, int kv_heads, int d, float base,
                             hipStream_t s);

@@ -129,6 +129,18 @@ def _i32(t):
     return t.to(torch.int32).contiguous()
 
 
+def launchCalPaddingoffset(input_lengths, max_q_len: int):
+    """-> (padding_offset [num_tokens], cum_seqlens [batch + 1]) (cal_paddingoffset.cu:51-86)."""
+    _dev(input_lengths)
+    lens = _i32(input_lengths)
+    n = int(lens.sum().item())
+    po = torch.empty(max(n, 1), device=lens.device, dtype=torch.int32)
+    cum = torch.empty(lens.numel() + 1, device=lens.device, dtype=torch.int32)
+    call("llmi_padding_offset", po.data_ptr(), cum.data_ptr(), lens.data_ptr(), lens.numel(), int(max_q_len),
+         _stream())
+    return po[:n], cum
+
+
 def launchAddFusedQKVBiasTransposeAndRoPE(qkv, padding_offset, history_length, batch: int, seq_len: int,
                                           heads: int, kv_heads: int, head_dim: int = 128, base: float = 10000.0):
     """qkv [num_tokens, (heads + 2 kv) * d] -> q [batch, heads, seq_len, d], k, v [batch, kv, seq_len, d]

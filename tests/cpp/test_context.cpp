@@ -57,16 +57,12 @@ int main(int argc, char** argv) {
         mk = std::max(mk, klens[b]);
         tokens += lens[b];
     }
-    // CalPaddingoffset (cal_paddingoffset.cu:51-72) on the host
-    std::vector<int> po;
-    for (int b = 0, cum = 0; b < bs; cum += mq - lens[b], ++b)
-        for (int i = 0; i < lens[b]; ++i) po.push_back(cum);
 
     const size_t nqkv = (size_t)tokens * (heads + 2 * kv) * hd;
     Dev<float> qkv(nqkv), q((size_t)bs * heads * mq * hd), k((size_t)bs * kv * mq * hd), v((size_t)bs * kv * mq * hd);
     Dev<float> kc((size_t)bs * kv * S * hd), vc((size_t)bs * kv * S * hd), mask((size_t)bs * mq * mk);
     Dev<float> qk((size_t)bs * heads * mq * mk), score((size_t)bs * heads * mq * mk), tout((size_t)tokens * heads * hd);
-    Dev<int> d_po(tokens), d_hist(bs), d_lens(bs), d_klens(bs);
+    Dev<int> d_po((size_t)bs * mq), d_cum(bs + 1), d_hist(bs), d_lens(bs), d_klens(bs);
     qkv.put(load(dir + "/in_qkv.bin", nqkv));
     qk.put(load(dir + "/in_qk.bin", qk.n));
     kc.put(std::vector<float>(kc.n, 0.f));
@@ -74,7 +70,6 @@ int main(int argc, char** argv) {
     q.put(std::vector<float>(q.n, 0.f));
     k.put(std::vector<float>(k.n, 0.f));
     v.put(std::vector<float>(v.n, 0.f));
-    d_po.put(po);
     d_hist.put(hist);
     d_lens.put(lens);
     d_klens.put(klens);
@@ -93,6 +88,8 @@ int main(int argc, char** argv) {
     params.rotary_embedding_dim = hd;
     params.rotary_embedding_base = 10000.f;
 
+    TensorWrapper<int> PO_FULL(GPU, INT32, {bs, mq}, d_po.p), CUM(GPU, INT32, {bs + 1}, d_cum.p);
+    launchCalPaddingoffset(&PO_FULL, &CUM, &LENS);
     launchAddFusedQKVBiasTransposeAndRoPE(&Q, &K, &V, &QKV, no_bias, &PO, &HIST, &LENS, params);
     launchConcatKVCache(&K, &V, &LAYER, &LENS, &HIST, &KC, &VC);
     launchBuildCausalMasks(&M, &LENS, &KLENS);
@@ -100,6 +97,11 @@ int main(int argc, char** argv) {
     launchTransposeOutRemovePadding(&Q, &PO, &TO);
     LLMI_CALL(llmi_device_sync());
 
+    {
+        std::vector<int> po = d_po.get(), cum = d_cum.get();
+        save(dir + "/out_po.bin", std::vector<float>(po.begin(), po.begin() + tokens));
+        save(dir + "/out_cum.bin", std::vector<float>(cum.begin(), cum.end()));
+    }
     save(dir + "/out_q.bin", q.get());
     save(dir + "/out_k.bin", k.get());
     save(dir + "/out_v.bin", v.get());

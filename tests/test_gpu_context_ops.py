@@ -194,3 +194,10 @@ def test_tp_allreduce_single_rank(ops, dt):
         comm.all_reduce(x)
         torch.cuda.synchronize()
     assert torch.equal(x, ref)
+
+
+def test_padding_offset_reference_example(ops):
+    """cal_paddingoffset.cu:13-25's worked example: lengths [5, 4, 7, 6], max_q_len 8."""
+    po, cum = ops.launchCalPaddingoffset(T(np.array([5, 4, 7, 6], np.int32)), 8)
+    np.testing.assert_array_equal(N(po).astype(np.int32), C.padding_offset([5, 4, 7, 6], 8))
+    assert N(cum).astype(int).tolist() == [0, 5, 9, 16, 22]
