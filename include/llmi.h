@@ -108,6 +108,29 @@ int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_d
  * greedy argmax over logits[n]; ties -> lowest index. out_id: device int32. */
 int llmi_argmax(const float* logits, int n, int32_t* out_id, llmi_stream_t stream);
 
+/* launchTopKforBeamSearch (src/kernels/topK.h:51-56, topK.cu:24-191): per row of
+ * logits [rows, vocab] (f32/f16), the k largest values in descending order -> topk_ids
+ * [rows, k] (device int32) and topk_vals [rows, k] (same dtype). Ties -> lower index
+ * (the reference's tie order follows its CUB reduction tree). k in [1, 16]; the
+ * reference fixes K = 5 (topK.cu:154). vocab < k pads with id -1, value 1e-20 (topK.h:15-20). */
+int llmi_topk(const void* logits, int dtype, int rows, int vocab, int k, int32_t* topk_ids, void* topk_vals,
+              llmi_stream_t stream);
+
+/* launchSampling (src/kernels/sampling.h:12-18, sampling.cu:28-115): for each row not yet
+ * finished, topk_vals <- exp(v - v[0]) in place, threshold u * sum, output_id = the first id
+ * whose running subtraction reaches <= 0 (% vocab), seqlen += 1, is_finished = (id == end_id).
+ * u in (0, 1] is drawn from llmi-prng-v1 seeded by step, stream = row (the reference uses
+ * curand XORWOW with the same seed/subsequence roles). is_finished: device uint8 (C++ bool). */
+int llmi_sampling(const int32_t* topk_ids, void* topk_vals, int dtype, int rows, int k, int32_t* output_id,
+                  int32_t* seqlen, uint8_t* is_finished, int step, int end_id, int vocab, llmi_stream_t stream);
+
+/* launchRepeatKVCache (src/kernels/repeat_kv.h, repeat_kv.cu:7-91): caches [layers, batch,
+ * kv_heads, max_seq, d] -> k_dst/v_dst [batch, heads, max_k_len, d], query head h reading kv
+ * head h / (heads / kv_heads), positions < context_length[b] only. */
+int llmi_repeat_kv(const void* k_cache, const void* v_cache, int dtype, int layer, const int32_t* context_length,
+                   int batch, int kv_heads, int max_seq, int heads, int max_k_len, int head_dim, void* k_dst,
+                   void* v_dst, llmi_stream_t stream);
+
 /* ---- context-phase (prefill) operators of the reference's unfused attention layer
  * (LLaMAContextAttentionLayer::forward, context_attention.cpp:108-161). The engine's
  * llmi_engine_prefill fuses them; these are the per-launcher equivalents. dtype is

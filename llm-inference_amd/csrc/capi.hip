@@ -104,6 +104,24 @@ int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_d
     return attn_decode_launch(a, STREAM(stream));
 }
 
+int llmi_topk(const void* logits, int dtype, int rows, int vocab, int k, int32_t* topk_ids, void* topk_vals,
+              llmi_stream_t stream) {
+    return topk_launch(logits, dtype, rows, vocab, k, topk_ids, topk_vals, STREAM(stream));
+}
+
+int llmi_sampling(const int32_t* topk_ids, void* topk_vals, int dtype, int rows, int k, int32_t* output_id,
+                  int32_t* seqlen, uint8_t* is_finished, int step, int end_id, int vocab, llmi_stream_t stream) {
+    return sampling_launch(topk_ids, topk_vals, dtype, rows, k, output_id, seqlen, is_finished, step, end_id, vocab,
+                           STREAM(stream));
+}
+
+int llmi_repeat_kv(const void* k_cache, const void* v_cache, int dtype, int layer, const int32_t* context_length,
+                   int batch, int kv_heads, int max_seq, int heads, int max_k_len, int head_dim, void* k_dst,
+                   void* v_dst, llmi_stream_t stream) {
+    return repeat_kv_launch(k_cache, v_cache, dtype, layer, context_length, batch, kv_heads, max_seq, heads,
+                            max_k_len, head_dim, k_dst, v_dst, STREAM(stream));
+}
+
 int llmi_padding_offset(int32_t* padding_offset, int32_t* cum_seqlens, const int32_t* input_lengths, int batch,
                         int max_q_len, llmi_stream_t stream) {
     return padding_offset_launch(padding_offset, cum_seqlens, input_lengths, batch, max_q_len, STREAM(stream));

@@ -11,6 +11,7 @@
 // All are memory-bound element moves or row reductions (fp32 arithmetic, T = float
 // or __half storage); roofline HBM, bytes = what they read + write.
 #include <cfloat>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -342,6 +343,71 @@ __global__ void padding_offset_kernel(int* po, int* cum, const int* lens, int ba
 int padding_offset_launch(int* po, int* cum, const int* lens, int batch, int max_q, hipStream_t s) {
     LLMI_REQUIRE(po && cum && lens && batch > 0 && max_q > 0, "padding_offset: bad arguments");
     hipLaunchKernelGGL(padding_offset_kernel, dim3(1), dim3(256), 0, s, po, cum, lens, batch, max_q);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace llmi
+
+// ------------------------------------------------ GQA repeat_kv
+namespace llmi {
+namespace {
+// repeat_value_cache (repeat_kv.cu:7-50): expand the layer's KV cache
+// [batch, kv_heads, max_seq, d] to [batch, heads, max_k_len, d] for the strided
+// batched matmuls, query head h reading kv head h / (heads / kv_heads). Only positions
+// < context_length[b] are written (the reference leaves the rest as they were).
+// One workgroup per (position chunk, batch, head); 16-B vectors along d when d allows.
+template <typename T, int V>
+__global__ void repeat_kv_kernel(const T* __restrict__ k_src, const T* __restrict__ v_src, T* __restrict__ k_dst,
+                                 T* __restrict__ v_dst, const int* __restrict__ ctx_len, size_t layer_off,
+                                 int kv_heads, int max_seq, int heads, int max_k, int d) {
+    using Vec = typename std::conditional<V == 1, T, uint4>::type;
+    const int b = blockIdx.y, h = blockIdx.z;
+    const int len = min(ctx_len[b], max_k);
+    const int dv = d / V;
+    const int kvh = h / (heads / kv_heads);
+    const size_t src = layer_off + ((size_t)b * kv_heads + kvh) * max_seq * d;
+    const size_t dst = ((size_t)b * heads + h) * max_k * d;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < len * dv; e += gridDim.x * blockDim.x) {
+        const size_t o = (size_t)(e / dv) * d + (size_t)(e % dv) * V;
+        *reinterpret_cast<Vec*>(k_dst + dst + o) = *reinterpret_cast<const Vec*>(k_src + src + o);
+        *reinterpret_cast<Vec*>(v_dst + dst + o) = *reinterpret_cast<const Vec*>(v_src + src + o);
+    }
+}
+
+template <typename T>
+void repeat_kv_go(const void* k, const void* v, void* kd, void* vd, const int* ctx, size_t off, int kv_heads,
+                  int max_seq, int heads, int max_k, int d, int batch, hipStream_t s) {
+    constexpr int V = 16 / sizeof(T);
+    const bool vec = d % V == 0;  // 16-B vectors along d; the reference's unit test uses d = 2
+    const int per = max_k * (vec ? d / V : d);
+    const dim3 grid((unsigned)std::min((per + 255) / 256, 64), (unsigned)batch, (unsigned)heads);
+    const T *ks = static_cast<const T*>(k), *vs = static_cast<const T*>(v);
+    T *kt = static_cast<T*>(kd), *vt = static_cast<T*>(vd);
+    if (vec)
+        hipLaunchKernelGGL((repeat_kv_kernel<T, V>), grid, dim3(256), 0, s, ks, vs, kt, vt, ctx, off, kv_heads,
+                           max_seq, heads, max_k, d);
+    else
+        hipLaunchKernelGGL((repeat_kv_kernel<T, 1>), grid, dim3(256), 0, s, ks, vs, kt, vt, ctx, off, kv_heads,
+                           max_seq, heads, max_k, d);
+}
+}  // namespace
+
+int repeat_kv_launch(const void* k_cache, const void* v_cache, int dtype, int layer, const int* ctx_len, int batch,
+                     int kv_heads, int max_seq, int heads, int max_k_len, int d, void* k_dst, void* v_dst,
+                     hipStream_t s) {
+    LLMI_REQUIRE(k_cache && v_cache && ctx_len && k_dst && v_dst && batch > 0 && kv_heads > 0 && heads > 0 &&
+                     max_seq > 0 && max_k_len > 0 && layer >= 0 && heads % kv_heads == 0,
+                 "repeat_kv: bad arguments");
+    LLMI_REQUIRE(dtype == LLMI_F32 || dtype == LLMI_F16, "repeat_kv: dtype must be f32 or f16");
+    LLMI_REQUIRE(d > 0, "repeat_kv: bad head_dim");
+    const size_t off = (size_t)layer * batch * kv_heads * max_seq * d;
+    if (dtype == LLMI_F32)
+        repeat_kv_go<float>(k_cache, v_cache, k_dst, v_dst, ctx_len, off, kv_heads, max_seq, heads, max_k_len, d,
+                            batch, s);
+    else
+        repeat_kv_go<__half>(k_cache, v_cache, k_dst, v_dst, ctx_len, off, kv_heads, max_seq, heads, max_k_len, d,
+                             batch, s);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }

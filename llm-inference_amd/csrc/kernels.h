@@ -304,6 +304,12 @@ int rope_decode_launch(float* qkv, int pos, int heads, int kv_heads, int head_di
                        hipStream_t s);
 int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long long* scratch,
                   hipStream_t s);
+int topk_launch(const void* logits, int dtype, int rows, int vocab, int k, int32_t* ids, void* vals, hipStream_t s);
+int sampling_launch(const int32_t* topk_ids, void* topk_vals, int dtype, int rows, int k, int32_t* output_id,
+                    int32_t* seqlen, uint8_t* is_finished, int step, int end_id, int vocab, hipStream_t s);
+int repeat_kv_launch(const void* k_cache, const void* v_cache, int dtype, int layer, const int* ctx_len, int batch,
+                     int kv_heads, int max_seq, int heads, int max_k_len, int d, void* k_dst, void* v_dst,
+                     hipStream_t s);
 
 // ---------------------------------------------------------- synthetic
 // in-place reduction over W rank buffers (device array of pointers); op 0 i64 sum, 1 f32 sum, 2 u64 max

@@ -1,0 +1,173 @@
+// Stochastic top-K sampling: the reference's
+// launchTopKforBeamSearch (src/kernels/topK.cu:24-191, topK.h:6-56) followed by
+// launchSampling (src/kernels/sampling.cu:28-115), as Llama<T>::Sampling wires them
+// (src/models/llama/llama.cpp:245-262). The engine's greedy path keeps its fused
+// argmax epilogue (K = 1 reduces to it); these launches serve callers that sample.
+//
+// topk: one workgroup of 1024 lanes per row. Every lane keeps a sorted K-list of the
+// values it strides over (coalesced, one HBM pass over the row), then K rounds of a
+// workgroup argmax over the lanes' heads pop the row's top K in order. Order is
+// value-descending with ties to the lower index -- the reference's heap is the same
+// sort but its tie order depends on the CUB reduction tree, so equal logits are the
+// one place the build is deterministic where the reference is not. Roofline: HBM,
+// rows * vocab * sizeof(T) bytes read; at batch 1 the row is 128 KB and the launch is
+// latency-bound (a few us), far below the 13 GB the token's GEMVs stream.
+//
+// sampling: one lane per row (K is small, the reference runs the whole loop on
+// tid 0 too). Semantics follow SamplingKernel (sampling.cu:28-84) exactly:
+// exp(v - v[0]) in place (stored as T), threshold = u * sum, first i whose running
+// subtraction reaches <= 0, ids taken % vocab, seqlen / is_finished update, rows already
+// finished untouched. The reference draws u with curand_uniform(XORWOW seeded by
+// step, subsequence = row); XORWOW's skip-ahead tables are not restated here, so u is
+// llmi-prng-v1: u = ((bits(tensor_key(step, SAMPLE), row) >> 40) + 1) * 2^-24 in (0, 1],
+// the same interval as curand_uniform. The oracle (oracle/sampling.py) uses the same
+// draw, so the selection is bit-exact against it.
+#include "kernels.h"
+#include "prng.h"
+
+namespace llmi {
+namespace {
+
+constexpr int kTopkThreads = 1024;
+constexpr uint32_t kSampleTid = 0x5A3Du;  // llmi-prng-v1 stream id of the sampling draw
+
+template <typename T> __device__ __forceinline__ float ldv(const T* p) { return (float)*p; }
+template <> __device__ __forceinline__ float ldv<__half>(const __half* p) { return __half2float(*p); }
+template <typename T> __device__ __forceinline__ void stv(T* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void stv<__half>(__half* p, float v) { *p = __float2half(v); }
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off, kWave);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+template <typename T, int K>
+__global__ __launch_bounds__(kTopkThreads) void topk_kernel(const T* __restrict__ logits, int vocab,
+                                                            int32_t* __restrict__ out_ids, T* __restrict__ out_vals) {
+    const T* row = logits + (size_t)blockIdx.x * vocab;
+    // lane-local sorted list, descending by argmax key; key 0 = empty slot
+    unsigned long long key[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) key[j] = 0ull;
+    for (int i = threadIdx.x; i < vocab; i += kTopkThreads) {
+        unsigned long long c = argmax_key(ldv(row + i), (uint32_t)i);
+        if (c > key[K - 1]) {
+            key[K - 1] = c;
+#pragma unroll
+            for (int j = K - 2; j >= 0; --j) {
+                if (key[j + 1] > key[j]) {
+                    const unsigned long long t = key[j];
+                    key[j] = key[j + 1];
+                    key[j + 1] = t;
+                }
+            }
+        }
+    }
+    __shared__ unsigned long long wbest[kTopkThreads / kWave];
+    const int lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
+    for (int r = 0; r < K; ++r) {
+        unsigned long long b = wave_max_u64(key[0]);
+        if (lane == 0) wbest[wid] = b;
+        __syncthreads();
+        b = lane < kTopkThreads / kWave ? wbest[lane] : 0ull;
+        b = wave_max_u64(b);
+        if (key[0] == b && b != 0ull) {  // keys are unique per index: exactly one lane pops
+#pragma unroll
+            for (int j = 0; j < K - 1; ++j) key[j] = key[j + 1];
+            key[K - 1] = 0ull;
+        }
+        if (threadIdx.x == 0) {
+            const size_t o = (size_t)blockIdx.x * K + r;
+            if (b == 0ull) {  // vocab < K: the reference's init() values (topK.h:15-20)
+                out_ids[o] = -1;
+                stv(out_vals + o, 1e-20f);
+            } else {
+                const uint32_t idx = argmax_key_index(b);
+                out_ids[o] = (int32_t)idx;
+                out_vals[o] = row[idx];  // the stored value itself, no float round trip
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <typename T>
+__global__ void sampling_kernel(const int32_t* __restrict__ topk_ids, T* __restrict__ topk_vals, int rows, int K,
+                                int32_t* __restrict__ output_id, int32_t* __restrict__ seqlen,
+                                uint8_t* __restrict__ is_finished, int step, int end_id, int vocab) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= rows || is_finished[b]) return;
+    T* v = topk_vals + (size_t)b * K;
+    const int32_t* id = topk_ids + (size_t)b * K;
+    const float mx = ldv(v);
+    float sum = 0.f;
+    for (int i = 0; i < K; ++i) {
+        stv(v + i, expf(ldv(v + i) - mx));
+        sum += ldv(v + i);
+    }
+    const uint64_t r = prng::bits(prng::tensor_key((uint64_t)(int64_t)step, kSampleTid), (uint64_t)b);
+    float thr = (float)((r >> 40) + 1ull) * 0x1p-24f * sum;
+    int out = id[0];
+    for (int i = 0; i < K; ++i) {
+        thr -= ldv(v + i);
+        if (thr <= 0.f) {
+            out = id[i] % vocab;
+            break;
+        }
+    }
+    output_id[b] = out;
+    seqlen[b] += 1;
+    is_finished[b] = out == end_id ? 1 : 0;
+}
+
+template <typename T>
+int topk_dispatch(const void* logits, int rows, int vocab, int k, int32_t* ids, void* vals, hipStream_t s) {
+    const T* x = static_cast<const T*>(logits);
+    T* y = static_cast<T*>(vals);
+    switch (k) {
+#define LLMI_TOPK_CASE(KK) \
+    case KK: hipLaunchKernelGGL((topk_kernel<T, KK>), dim3(rows), dim3(kTopkThreads), 0, s, x, vocab, ids, y); break;
+        LLMI_TOPK_CASE(1) LLMI_TOPK_CASE(2) LLMI_TOPK_CASE(3) LLMI_TOPK_CASE(4) LLMI_TOPK_CASE(5)
+        LLMI_TOPK_CASE(6) LLMI_TOPK_CASE(7) LLMI_TOPK_CASE(8) LLMI_TOPK_CASE(9) LLMI_TOPK_CASE(10)
+        LLMI_TOPK_CASE(11) LLMI_TOPK_CASE(12) LLMI_TOPK_CASE(13) LLMI_TOPK_CASE(14) LLMI_TOPK_CASE(15)
+        LLMI_TOPK_CASE(16)
+#undef LLMI_TOPK_CASE
+        default: return LLMI_EINVAL;
+    }
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace
+
+int topk_launch(const void* logits, int dtype, int rows, int vocab, int k, int32_t* ids, void* vals, hipStream_t s) {
+    LLMI_REQUIRE(logits && ids && vals && rows > 0 && vocab > 0, "topk: bad arguments");
+    LLMI_REQUIRE(k >= 1 && k <= 16, "topk: k must be in [1, 16]");
+    LLMI_REQUIRE(dtype == LLMI_F32 || dtype == LLMI_F16, "topk: dtype must be f32 or f16");
+    return dtype == LLMI_F32 ? topk_dispatch<float>(logits, rows, vocab, k, ids, vals, s)
+                           : topk_dispatch<__half>(logits, rows, vocab, k, ids, vals, s);
+}
+
+int sampling_launch(const int32_t* topk_ids, void* topk_vals, int dtype, int rows, int k, int32_t* output_id,
+                    int32_t* seqlen, uint8_t* is_finished, int step, int end_id, int vocab, hipStream_t s) {
+    LLMI_REQUIRE(topk_ids && topk_vals && output_id && seqlen && is_finished && rows > 0 && k >= 1 && vocab > 0,
+                 "sampling: bad arguments");
+    LLMI_REQUIRE(dtype == LLMI_F32 || dtype == LLMI_F16, "sampling: dtype must be f32 or f16");
+    const int grid = (rows + kWave - 1) / kWave;
+    if (dtype == LLMI_F32)
+        hipLaunchKernelGGL(sampling_kernel<float>, dim3(grid), dim3(kWave), 0, s, topk_ids,
+                           static_cast<float*>(topk_vals), rows, k, output_id, seqlen, is_finished, step, end_id,
+                           vocab);
+    else
+        hipLaunchKernelGGL(sampling_kernel<__half>, dim3(grid), dim3(kWave), 0, s, topk_ids,
+                           static_cast<__half*>(topk_vals), rows, k, output_id, seqlen, is_finished, step, end_id,
+                           vocab);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace llmi

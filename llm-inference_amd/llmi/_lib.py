@@ -47,6 +47,9 @@ _SIGS = {
     "llmi_attn_workspace_bytes": (_SZ, [_I, _I, _I]),
     "llmi_attn_decode": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P]),
     "llmi_argmax": (_I, [_P, _I, _P, _P]),
+    "llmi_topk": (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
+    "llmi_sampling": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P]),
+    "llmi_repeat_kv": (_I, [_P, _P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "llmi_padding_offset": (_I, [_P, _P, _P, _I, _I, _P]),
     "llmi_rope_qkv_prefill": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P]),
     "llmi_kv_append": (_I, [_P, _P, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

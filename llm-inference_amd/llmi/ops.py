@@ -117,6 +117,47 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def launchTopKforBeamSearch(probs: torch.Tensor, k: int = 5):
+    """probs [rows, vocab] f32/f16 -> (final_topk_ids int32 [rows, k], final_topk_vals [rows, k]),
+    descending (topK.cu:24-191; the reference fixes K = 5, topK.cu:154). One launch: the
+    reference's round-1 / round-2 scratch buffers are not needed."""
+    _dev(probs)
+    x = probs.contiguous().view(-1, probs.shape[-1])
+    ids = torch.empty(x.shape[0], k, device=x.device, dtype=torch.int32)
+    vals = torch.empty(x.shape[0], k, device=x.device, dtype=x.dtype)
+    call("llmi_topk", x.data_ptr(), _dt(x), x.shape[0], x.shape[1], int(k), ids.data_ptr(), vals.data_ptr(),
+         _stream())
+    return ids, vals
+
+
+def launchSampling(topk_id, topk_val, seqlen, is_finished, output_id, step: int, end_id: int, vocab_size: int):
+    """In place, like the reference (sampling.cu:87-115, params step/end_id/vocab_size from
+    its IntDict): topk_val <- exp(v - v[0]); output_id, seqlen, is_finished (uint8/bool)
+    updated for unfinished rows."""
+    _dev(topk_id, topk_val, seqlen, is_finished, output_id)
+    for t, dt in ((topk_id, torch.int32), (seqlen, torch.int32), (output_id, torch.int32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError("launchSampling: ids, seqlen and output_id must be contiguous int32")
+    if is_finished.dtype not in (torch.bool, torch.uint8) or not topk_val.is_contiguous():
+        raise ValueError("launchSampling: is_finished must be bool/uint8, topk_val contiguous")
+    rows, k = topk_id.shape
+    call("llmi_sampling", topk_id.data_ptr(), topk_val.data_ptr(), _dt(topk_val), rows, k, output_id.data_ptr(),
+         seqlen.data_ptr(), is_finished.data_ptr(), int(step), int(end_id), int(vocab_size), _stream())
+    return output_id
+
+
+def launchRepeatKVCache(k_cache_src, v_cache_src, context_length, layer: int, k_cache_dst, v_cache_dst):
+    """caches [layers, batch, kv_heads, max_seq, d] -> dst [batch, heads, max_k_len, d]
+    (repeat_kv.cu:52-91); positions >= context_length[b] are left as they were."""
+    _dev(k_cache_src, v_cache_src, context_length, k_cache_dst, v_cache_dst)
+    _, b, kv, max_seq, d = k_cache_src.shape
+    heads, max_k = k_cache_dst.shape[1], k_cache_dst.shape[2]
+    ctx = _i32(context_length)
+    call("llmi_repeat_kv", k_cache_src.data_ptr(), v_cache_src.data_ptr(), _dt(k_cache_src), int(layer),
+         ctx.data_ptr(), b, kv, max_seq, heads, max_k, d, k_cache_dst.data_ptr(), v_cache_dst.data_ptr(), _stream())
+    return k_cache_dst, v_cache_dst
+
+
 def synth_fill(out: torch.Tensor, kind: int, seed: int, tid: int, rows: int, cols: int,
                row0: int = 0, col0: int = 0, ld: int = 0) -> torch.Tensor:
     _dev(out)
