@@ -140,6 +140,37 @@ inline void launchTopKforBeamSearch(TensorWrapper<float>* probs, TensorWrapper<i
     LLMI_CALL(llmi_argmax(probs->data, probs->shape.back(), final_topk_id->data, stream));
 }
 
+// topK.h:51-56 -- the reference's full signature. topk_ids / topK_values are the
+// reference's round-1 scratch [bs, beam, BlockPerBeam, K]; the build selects in one
+// launch and leaves them untouched. K = final_topk_ids->shape.back() (the reference
+// fixes 5). Values descending, ties -> lower index (include/llmi.h: llmi_topk).
+template <typename T>
+void launchTopKforBeamSearch(TensorWrapper<T>* probs, TensorWrapper<int>* topk_ids, TensorWrapper<T>* topK_values,
+                             TensorWrapper<int>* final_topk_ids, TensorWrapper<T>* final_topk_values,
+                             void* stream = nullptr) {
+    (void)topk_ids;
+    (void)topK_values;
+    const int vocab = probs->shape.back(), rows = probs->size() / vocab;
+    const int k = final_topk_ids->shape.back();
+    LLM_CHECK_WITH_INFO(final_topk_values->size() == rows * k && final_topk_ids->size() == rows * k,
+                        "topk: final buffers must be [bs * beam, K]");
+    LLMI_CALL(llmi_topk(probs->data, llmiDtype(getTensorType<T>()), rows, vocab, k, final_topk_ids->data,
+                        final_topk_values->data, stream));
+}
+
+// sampling.h:12-18 -- params "step" (the draw's seed), "end_id", "vocab_size"
+// (sampling.cu:92-95); topk_val is overwritten with exp(v - v[0]) as in the reference.
+template <typename T>
+void launchSampling(TensorWrapper<int>* topk_id, TensorWrapper<T>* topk_val, TensorWrapper<int>* seqlen,
+                    TensorWrapper<bool>* is_finished, TensorWrapper<int>* output_id, IntDict& params,
+                    void* stream = nullptr) {
+    LLM_CHECK_WITH_INFO(topk_id->shape.size() == 2, "sampling: topk_id must be [bs, K]");
+    LLMI_CALL(llmi_sampling(topk_id->data, topk_val->data, llmiDtype(getTensorType<T>()), topk_id->shape[0],
+                            topk_id->shape[1], output_id->data, seqlen->data,
+                            reinterpret_cast<uint8_t*>(is_finished->data), params.at("step"), params.at("end_id"),
+                            params.at("vocab_size"), stream));
+}
+
 // ---- context-phase launchers (prefill; the engine fuses them, see llmi_engine_prefill).
 // T = float or half_t storage; padding_offset, history_length, input_length, q_lens,
 // k_lens, cur_query_length are device int tensors; layer_id is a host tensor.
@@ -223,6 +254,19 @@ void launchLinearStridedBatchGemm(TensorWrapper<T>* input1, TensorWrapper<T>* in
     LLM_CHECK_WITH_INFO(output->shape[2] == m && output->shape[3] == n, "strided batch gemm: bad output shape");
     LLMI_CALL(llmi_batched_matmul(input1->data, input2->data, output->data, llmiDtype(getTensorType<T>()), batch, m, n,
                                   k, trans_a ? 1 : 0, trans_b ? 1 : 0, cublas_wrapper ? cublas_wrapper->stream : nullptr));
+}
+
+// repeat_kv.h -- caches [layers, bs, kv_heads, max_seq, head] -> k/v_cache_dst
+// [bs, heads, max_k_len, head]; positions < context_length[b] (device int) are written.
+template <typename T>
+void launchRepeatKVCache(TensorWrapper<T>* k_cache_src, TensorWrapper<T>* v_cache_src,
+                         TensorWrapper<int>* context_length, TensorWrapper<int>* layer_id,
+                         TensorWrapper<T>* k_cache_dst, TensorWrapper<T>* v_cache_dst, void* stream = nullptr) {
+    LLM_CHECK_WITH_INFO(k_cache_src->shape.size() == 5 && k_cache_dst->shape.size() == 4, "repeat kv: bad shapes");
+    LLMI_CALL(llmi_repeat_kv(k_cache_src->data, v_cache_src->data, llmiDtype(getTensorType<T>()), layer_id->getVal(),
+                             context_length->data, context_length->shape[0], k_cache_src->shape[2],
+                             k_cache_src->shape[3], k_cache_dst->shape[1], k_cache_dst->shape[2],
+                             k_cache_dst->shape[3], k_cache_dst->data, v_cache_dst->data, stream));
 }
 
 // cal_paddingoffset.h -- padding_offset [batch, max_q_len] (its first num_tokens entries

@@ -92,10 +92,46 @@ int main(int argc, char** argv) {
     launchCalPaddingoffset(&PO_FULL, &CUM, &LENS);
     launchAddFusedQKVBiasTransposeAndRoPE(&Q, &K, &V, &QKV, no_bias, &PO, &HIST, &LENS, params);
     launchConcatKVCache(&K, &V, &LAYER, &LENS, &HIST, &KC, &VC);
+    Dev<float> kr((size_t)bs * heads * mk * hd), vr((size_t)bs * heads * mk * hd);
+    kr.put(std::vector<float>(kr.n, 0.f));
+    vr.put(std::vector<float>(vr.n, 0.f));
+    TensorWrapper<float> KR(GPU, FP32, {bs, heads, mk, hd}, kr.p), VR(GPU, FP32, {bs, heads, mk, hd}, vr.p);
+    launchRepeatKVCache(&KC, &VC, &KLENS, &LAYER, &KR, &VR);  // context_attention.cpp:136
     launchBuildCausalMasks(&M, &LENS, &KLENS);
     launchScaleMaskAndSoftmax(&QK, &M, &SC, 1.0f / std::sqrt((float)hd));
     launchTransposeOutRemovePadding(&Q, &PO, &TO);
+    // top-K + sampling over the rows of qk ([bs * heads * mq, mk], K = 5) as Llama<T>::Sampling
+    const int rows = bs * heads * mq, TOPK = 5;
+    Dev<int> tid(rows * TOPK), oid(rows), seql(rows);
+    Dev<float> tval(rows * TOPK);
+    Dev<uint8_t> fin(rows);
+    std::vector<uint8_t> fin_h(rows, 0);
+    for (int r = 0; r < rows; r += 7) fin_h[r] = 1;
+    fin.put(fin_h);
+    seql.put(std::vector<int>(rows, 4));
+    oid.put(std::vector<int>(rows, -1));
+    TensorWrapper<float> PROBS(GPU, FP32, {rows, mk}, qk.p), TVAL(GPU, FP32, {rows, TOPK}, tval.p);
+    TensorWrapper<int> TID(GPU, INT32, {rows, TOPK}, tid.p), OID(GPU, INT32, {rows}, oid.p), SEQ(GPU, INT32, {rows}, seql.p);
+    TensorWrapper<bool> FIN(GPU, BOOL, {rows}, reinterpret_cast<bool*>(fin.p));
+    launchTopKforBeamSearch(&PROBS, &TID, &TVAL, &TID, &TVAL);
     LLMI_CALL(llmi_device_sync());
+    {
+        std::vector<int> t = tid.get();
+        save(dir + "/out_topk_ids.bin", std::vector<float>(t.begin(), t.end()));
+        save(dir + "/out_topk_vals.bin", tval.get());
+    }
+    IntDict sp{{"step", 3}, {"end_id", 2}, {"vocab_size", mk}};
+    launchSampling(&TID, &TVAL, &SEQ, &FIN, &OID, sp);
+    LLMI_CALL(llmi_device_sync());
+    {
+        std::vector<int> o = oid.get(), sq = seql.get();
+        std::vector<uint8_t> f = fin.get();
+        save(dir + "/out_sample_id.bin", std::vector<float>(o.begin(), o.end()));
+        save(dir + "/out_sample_seq.bin", std::vector<float>(sq.begin(), sq.end()));
+        save(dir + "/out_sample_fin.bin", std::vector<float>(f.begin(), f.end()));
+    }
+    save(dir + "/out_kr.bin", kr.get());
+    save(dir + "/out_vr.bin", vr.get());
 
     {
         std::vector<int> po = d_po.get(), cum = d_cum.get();
