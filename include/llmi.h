@@ -257,6 +257,15 @@ int llmi_engine_create(const llmi_config* cfg, int device, const void* tp_id, ll
 int llmi_engine_destroy(llmi_engine* e);
 /* Llama<T>::loadWeightsFromDummy (src/models/llama/llama.h) with llmi-prng-v1 weights. */
 int llmi_engine_load_synthetic(llmi_engine* e, uint64_t seed);
+/* LlamaWeight<T>::loadWeights(weight_path) (llama_weights.cc:41-53, layer_weights.cc:48-66,
+ * loadWeightFromBin weight_utils.cu:90-187): reads weight_path + "<name>.bin", raw fp32, for
+ * model.embed_tokens.weight, lm_head.weight, model.norm.weight and per layer l
+ * model.layers.<l>.{input_layernorm, post_attention_layernorm, self_attn.qkv, self_attn.o_proj,
+ * mlp.gate_up_proj, mlp.down_proj}.weight (unsharded shapes; this rank's slice is taken).
+ * fp32 -> fp16 is round-to-nearest-even. int8 engines are refused (no reference format). */
+int llmi_engine_load_bin(llmi_engine* e, const char* weight_path);
+/* One tensor of the same set from a host fp32 buffer (name without ".bin"; count checked). */
+int llmi_engine_load_tensor(llmi_engine* e, const char* name, const float* host, size_t count);
 /* Reset the sequence and stage a prompt (device copy). */
 int llmi_engine_set_prompt(llmi_engine* e, const int32_t* ids, int n);
 /* Run n forward steps (one token each). use_graph: replay the captured hipGraph. */
@@ -315,6 +324,7 @@ typedef struct llmi_group llmi_group;
 int llmi_group_create(const llmi_config* cfg, int world, int device, llmi_group** out);
 int llmi_group_destroy(llmi_group* g);
 int llmi_group_load_synthetic(llmi_group* g, uint64_t seed);
+int llmi_group_load_bin(llmi_group* g, const char* weight_path);
 int llmi_group_set_prompt(llmi_group* g, const int32_t* ids, int n);
 int llmi_group_decode(llmi_group* g, int n_steps, int use_graph);
 /* tokens as seen by one rank (every rank must agree) */

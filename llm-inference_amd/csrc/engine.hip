@@ -356,6 +356,141 @@ struct Engine {
         return LLMI_OK;
     }
 
+    // ------------------------------------------------ weights from the reference's files
+    // LlamaWeight<T>::loadWeights / LlamaLayerWeight<T>::loadWeights (llama_weights.cc:41-53,
+    // layer_weights.cc:48-66) with loadWeightFromBin<T, float> (weight_utils.cu:90-187): one
+    // raw fp32 file per (unsharded) tensor, fused qkv [(heads + 2 kv) * d, H] and gate_up
+    // [2 I, H]. The host converts to the engine's dtype (RNE, like the reference's
+    // fp32 -> half cast) and copies this rank's slice: q/k/v and gate/up rows, o/down
+    // columns, lm_head rows (the layout load_synthetic fills).
+    static int put_host(void* dst, int dt, const float* src, size_t src_ld, int rows, int cols, size_t row0,
+                        size_t col0, hipStream_t s) {
+        const size_t n = (size_t)rows * cols, es = dtype_size(dt);
+        std::vector<uint8_t> h(n * es);
+        for (int r = 0; r < rows; ++r) {
+            const float* a = src + (row0 + r) * src_ld + col0;
+            if (dt == LLMI_F32) {
+                std::memcpy(h.data() + (size_t)r * cols * 4, a, (size_t)cols * 4);
+            } else {
+                _Float16* o = reinterpret_cast<_Float16*>(h.data()) + (size_t)r * cols;
+                for (int c2 = 0; c2 < cols; ++c2) o[c2] = (_Float16)a[c2];
+            }
+        }
+        LLMI_HIP(hipMemcpyAsync(dst, h.data(), h.size(), hipMemcpyHostToDevice, s));
+        LLMI_HIP(hipStreamSynchronize(s));  // h is released on return
+        return LLMI_OK;
+    }
+
+    // name: the reference's file stem without ".bin" (e.g. "model.layers.3.self_attn.qkv.weight")
+    int load_tensor(const char* name, const float* src, size_t count) {
+        LLMI_REQUIRE(name && src, "load_tensor: null argument");
+        const std::string nm(name);
+        const size_t H = c.hidden, D = c.head_dim, QR = (size_t)c.heads * D, KR = (size_t)c.kv_heads * D;
+        const size_t I = c.inter, r = c.tp_rank;
+        auto need = [&](size_t n) -> int {
+            if (count != n) {
+                set_last_error("[llmi][ERROR] load_tensor: " + nm + " has " + std::to_string(count) + " values, expected " +
+                          std::to_string(n));
+                return LLMI_EINVAL;
+            }
+            return LLMI_OK;
+        };
+        auto lin_ok = [&]() -> int {
+            LLMI_REQUIRE(wdt != LLMI_I8, "load_tensor: int8 engines take synthetic weights only "
+                                         "(the reference's .bin format is fp32; W8A16 is build-defined)");
+            return LLMI_OK;
+        };
+        if (nm == "model.embed_tokens.weight") {
+            LLMI_TRY(need((size_t)c.vocab * H));
+            return put_host(embed, edt, src, H, c.vocab, (int)H, 0, 0, stream);
+        }
+        if (nm == "lm_head.weight") {
+            LLMI_TRY(need((size_t)c.vocab * H));
+            return put_host(lm_head, edt, src, H, vl, (int)H, r * vl, 0, stream);
+        }
+        if (nm == "model.norm.weight") {
+            LLMI_TRY(need(H));
+            return put_host(final_norm, edt, src, H, 1, (int)H, 0, 0, stream);
+        }
+        const std::string pre = "model.layers.";
+        LLMI_REQUIRE(nm.compare(0, pre.size(), pre) == 0, ("load_tensor: unknown tensor " + nm).c_str());
+        size_t dot = nm.find('.', pre.size());
+        LLMI_REQUIRE(dot != std::string::npos, ("load_tensor: unknown tensor " + nm).c_str());
+        const int l = std::atoi(nm.substr(pre.size(), dot - pre.size()).c_str());
+        LLMI_REQUIRE(l >= 0 && l < c.layers, ("load_tensor: layer out of range in " + nm).c_str());
+        const std::string leaf = nm.substr(dot + 1);
+        Layer& L = layers[l];
+        const size_t ws = dtype_size(wdt);
+        if (leaf == "input_layernorm.weight" || leaf == "post_attention_layernorm.weight") {
+            LLMI_TRY(need(H));
+            return put_host(leaf[0] == 'i' ? L.attn_norm : L.ffn_norm, edt, src, H, 1, (int)H, 0, 0, stream);
+        }
+        if (leaf == "self_attn.qkv.weight") {
+            LLMI_TRY(lin_ok());
+            LLMI_TRY(need((QR + 2 * KR) * H));
+            char* d = (char*)L.qkv;
+            LLMI_TRY(put_host(d, wdt, src, H, ql, (int)H, r * ql, 0, stream));
+            LLMI_TRY(put_host(d + (size_t)ql * H * ws, wdt, src, H, kvrows, (int)H, QR + r * kvrows, 0, stream));
+            return put_host(d + (size_t)(ql + kvrows) * H * ws, wdt, src, H, kvrows, (int)H, QR + KR + r * kvrows,
+                            0, stream);
+        }
+        if (leaf == "self_attn.o_proj.weight") {
+            LLMI_TRY(lin_ok());
+            LLMI_TRY(need(H * QR));
+            return put_host(L.o, wdt, src, QR, (int)H, ql, 0, r * ql, stream);
+        }
+        if (leaf == "mlp.gate_up_proj.weight") {
+            LLMI_TRY(lin_ok());
+            LLMI_TRY(need(2 * I * H));
+            LLMI_TRY(put_host(L.gu, wdt, src, H, il, (int)H, r * il, 0, stream));
+            return put_host((char*)L.gu + (size_t)il * H * ws, wdt, src, H, il, (int)H, I + r * il, 0, stream);
+        }
+        if (leaf == "mlp.down_proj.weight") {
+            LLMI_TRY(lin_ok());
+            LLMI_TRY(need(H * I));
+            return put_host(L.down, wdt, src, I, (int)H, il, 0, r * il, stream);
+        }
+        set_last_error("[llmi][ERROR] load_tensor: unknown tensor " + nm);
+        return LLMI_EINVAL;
+    }
+
+    // Llama<T>::loadWeights(weight_path): weight_path + "<name>.bin" for every tensor.
+    int load_bin(const char* weight_path) {
+        LLMI_REQUIRE(weight_path, "load_bin: null path");
+        std::vector<std::string> names = {"model.norm.weight", "lm_head.weight", "model.embed_tokens.weight"};
+        for (int l = 0; l < c.layers; ++l)
+            for (const char* leaf : {"input_layernorm.weight", "post_attention_layernorm.weight",
+                                     "self_attn.qkv.weight", "self_attn.o_proj.weight", "mlp.gate_up_proj.weight",
+                                     "mlp.down_proj.weight"})
+                names.push_back("model.layers." + std::to_string(l) + "." + leaf);
+        std::vector<float> buf;
+        for (const std::string& nm : names) {
+            const std::string path = std::string(weight_path) + nm + ".bin";
+            FILE* f = std::fopen(path.c_str(), "rb");
+            if (!f) {
+                set_last_error("[llmi][ERROR] load_bin: cannot open " + path);
+                return LLMI_EINVAL;
+            }
+            std::fseek(f, 0, SEEK_END);
+            const long bytes = std::ftell(f);
+            std::fseek(f, 0, SEEK_SET);
+            if (bytes < 0 || bytes % 4 != 0) {
+                std::fclose(f);
+                set_last_error("[llmi][ERROR] load_bin: " + path + " is not an fp32 file");
+                return LLMI_EINVAL;
+            }
+            buf.resize((size_t)bytes / 4);
+            const size_t got = std::fread(buf.data(), 4, buf.size(), f);
+            std::fclose(f);
+            if (got != buf.size()) {
+                set_last_error("[llmi][ERROR] load_bin: short read on " + path);
+                return LLMI_EINVAL;
+            }
+            LLMI_TRY(load_tensor(nm.c_str(), buf.data(), buf.size()));
+        }
+        return LLMI_OK;
+    }
+
     // ---------------------------------------------------------- one token
     GemvArgs lm_args(bool from_x = false) const {
         GemvArgs a;
@@ -1003,6 +1138,18 @@ int llmi_engine_load_synthetic(llmi_engine* e, uint64_t seed) {
     return e->e.load_synthetic(seed);
 }
 
+int llmi_engine_load_tensor(llmi_engine* e, const char* name, const float* host, size_t count) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.load_tensor(name, host, count);
+}
+
+int llmi_engine_load_bin(llmi_engine* e, const char* weight_path) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.load_bin(weight_path);
+}
+
 int llmi_engine_set_prompt(llmi_engine* e, const int32_t* ids, int n) {
     LLMI_REQUIRE(e, "null engine");
     LLMI_HIP(hipSetDevice(e->e.device));
@@ -1250,6 +1397,15 @@ int llmi_group_destroy(llmi_group* g) {
 int llmi_group_load_synthetic(llmi_group* g, uint64_t seed) {
     LLMI_REQUIRE(g, "null group");
     for (auto& e : g->g.r) LLMI_TRY(e->load_synthetic(seed));
+    return LLMI_OK;
+}
+
+int llmi_group_load_bin(llmi_group* g, const char* weight_path) {
+    LLMI_REQUIRE(g, "null group");
+    for (auto& e : g->g.r) {
+        LLMI_HIP(hipSetDevice(e->device));
+        LLMI_TRY(e->load_bin(weight_path));
+    }
     return LLMI_OK;
 }
 

@@ -72,6 +72,8 @@ _SIGS = {
     "llmi_engine_create": (_I, [C.POINTER(Config), _I, _P, C.POINTER(_P)]),
     "llmi_engine_destroy": (_I, [_P]),
     "llmi_engine_load_synthetic": (_I, [_P, _U64]),
+    "llmi_engine_load_bin": (_I, [_P, C.c_char_p]),
+    "llmi_engine_load_tensor": (_I, [_P, C.c_char_p, _P, _SZ]),
     "llmi_engine_set_prompt": (_I, [_P, _P, _I]),
     "llmi_engine_decode": (_I, [_P, _I, _I]),
     "llmi_engine_prefill": (_I, [_P, _I, _I]),
@@ -88,6 +90,7 @@ _SIGS = {
     "llmi_group_create": (_I, [C.POINTER(Config), _I, _I, C.POINTER(_P)]),
     "llmi_group_destroy": (_I, [_P]),
     "llmi_group_load_synthetic": (_I, [_P, _U64]),
+    "llmi_group_load_bin": (_I, [_P, C.c_char_p]),
     "llmi_group_set_prompt": (_I, [_P, _P, _I]),
     "llmi_group_decode": (_I, [_P, _I, _I]),
     "llmi_group_tokens": (_I, [_P, _I, _P, _I, C.POINTER(_I)]),

@@ -65,6 +65,15 @@ class Engine:
     def load_synthetic(self, seed: int):
         call("llmi_engine_load_synthetic", self._h, seed)
 
+    def load_bin(self, weight_path: str):
+        """Llama<T>::loadWeights(weight_path): weight_path + "<name>.bin" raw fp32 files
+        (llmi/convert.py writes them); the path is used as a prefix, like the reference's."""
+        call("llmi_engine_load_bin", self._h, weight_path.encode())
+
+    def load_tensor(self, name: str, values: np.ndarray):
+        v = np.ascontiguousarray(values, dtype=np.float32)
+        call("llmi_engine_load_tensor", self._h, name.encode(), v.ctypes.data, v.size)
+
     def set_prompt(self, ids):
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         call("llmi_engine_set_prompt", self._h, ids.ctypes.data, len(ids))
@@ -174,6 +183,9 @@ class TPGroup:
 
     def load_synthetic(self, seed: int):
         call("llmi_group_load_synthetic", self._h, seed)
+
+    def load_bin(self, weight_path: str):
+        call("llmi_group_load_bin", self._h, weight_path.encode())
 
     def tokens(self, rank: int = 0, n: Optional[int] = None) -> np.ndarray:
         n = self.cfg.max_seq + 1 if n is None else n
