@@ -266,6 +266,12 @@ int llmi_engine_load_synthetic(llmi_engine* e, uint64_t seed);
 int llmi_engine_load_bin(llmi_engine* e, const char* weight_path);
 /* One tensor of the same set from a host fp32 buffer (name without ".bin"; count checked). */
 int llmi_engine_load_tensor(llmi_engine* e, const char* name, const float* host, size_t count);
+/* Llama<T>::Sampling (llama.cpp:245-262: launchTopKforBeamSearch + launchSampling) inside the
+ * decode step: k in [1, 16] samples each generated token from the top k logits with
+ * sampling.cu's rule, u drawn from llmi-prng-v1 at step = seed + (position of the token);
+ * k = 0 restores greedy argmax (the default). Needs tp_world == 1. Applies to tokens chosen
+ * by decode steps (a batched prefill's first token stays greedy). */
+int llmi_engine_set_sampling(llmi_engine* e, int k, uint64_t seed);
 /* Reset the sequence and stage a prompt (device copy). */
 int llmi_engine_set_prompt(llmi_engine* e, const int32_t* ids, int n);
 /* Run n forward steps (one token each). use_graph: replay the captured hipGraph. */

@@ -112,8 +112,15 @@ struct Engine {
     int host_next_pos = 0, prompt_len = 0;
     unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
     uint64_t seed = 0;
+    // stochastic sampling (Llama<T>::Sampling, llama.cpp:245-262): 0 = greedy argmax
+    int sample_k = 0;
+    uint64_t sample_seed = 0;
+    int32_t* samp_ids = nullptr;
+    float* samp_vals = nullptr;
 
     ~Engine() {  // teardown errors are not actionable; ignore them explicitly
+        if (samp_ids) (void)hipFree(samp_ids);
+        if (samp_vals) (void)hipFree(samp_vals);
         if (exec) (void)hipGraphExecDestroy(exec);
         if (graph) (void)hipGraphDestroy(graph);
         if (comm) (void)ncclCommDestroy(comm);
@@ -679,7 +686,33 @@ struct Engine {
         LLMI_TRY(gemv_launch(gu_args(l), stream));
         return gemv_launch(down_args(l), stream);
     }
-    int rec_head() { return gemv_launch(lm_args(), stream); }
+    int rec_head() {
+        LLMI_TRY(gemv_launch(lm_args(), stream));
+        if (sample_k == 0) return LLMI_OK;
+        // top-K of this token's logits, then the sampled id replaces the argmax partials
+        LLMI_TRY(topk_launch(logits, LLMI_F32, 1, c.vocab, sample_k, samp_ids, samp_vals, stream));
+        return sample_pick_launch(st, samp_ids, samp_vals, sample_k, sample_seed, partials, lm_grid, stream);
+    }
+
+    int set_sampling(int k, uint64_t sd) {
+        LLMI_REQUIRE(k >= 0 && k <= 16, "set_sampling: k must be in [0, 16] (0 = greedy)");
+        LLMI_REQUIRE(k == 0 || (c.tp_world == 1 && !grouped), "set_sampling: sampling needs the full logits (tp_world 1)");
+        if (k > 0 && !samp_ids) {
+            LLMI_HIP(hipMalloc(&samp_ids, 16 * sizeof(int32_t)));
+            LLMI_HIP(hipMalloc(&samp_vals, 16 * sizeof(float)));
+        }
+        if (exec) {  // the captured step changes: re-capture on the next graph decode
+            LLMI_HIP(hipGraphExecDestroy(exec));
+            exec = nullptr;
+        }
+        if (graph) {
+            LLMI_HIP(hipGraphDestroy(graph));
+            graph = nullptr;
+        }
+        sample_k = k;
+        sample_seed = sd;
+        return LLMI_OK;
+    }
 
     int record_step() {
         LLMI_REQUIRE(!grouped, "engine: a group rank is stepped by its group");
@@ -1142,6 +1175,12 @@ int llmi_engine_load_tensor(llmi_engine* e, const char* name, const float* host,
     LLMI_REQUIRE(e, "null engine");
     LLMI_HIP(hipSetDevice(e->e.device));
     return e->e.load_tensor(name, host, count);
+}
+
+int llmi_engine_set_sampling(llmi_engine* e, int k, uint64_t seed) {
+    LLMI_REQUIRE(e, "null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.set_sampling(k, seed);
 }
 
 int llmi_engine_load_bin(llmi_engine* e, const char* weight_path) {

@@ -304,6 +304,11 @@ int rope_decode_launch(float* qkv, int pos, int heads, int kv_heads, int head_di
                        hipStream_t s);
 int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long long* scratch,
                   hipStream_t s);
+// engine sampling: u from llmi-prng-v1 with step = seed + (cur_pos + 1) (the position the
+// token is chosen for), sampling.cu's rule over the top-K, result written as the only
+// non-zero argmax partial so step_start / finalize pick it.
+int sample_pick_launch(const struct DecodeState* st, const int32_t* ids, float* vals, int k, uint64_t seed,
+                       unsigned long long* partials, int np, hipStream_t s);
 int topk_launch(const void* logits, int dtype, int rows, int vocab, int k, int32_t* ids, void* vals, hipStream_t s);
 int sampling_launch(const int32_t* topk_ids, void* topk_vals, int dtype, int rows, int k, int32_t* output_id,
                     int32_t* seqlen, uint8_t* is_finished, int step, int end_id, int vocab, hipStream_t s);

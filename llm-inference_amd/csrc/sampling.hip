@@ -124,6 +124,31 @@ __global__ void sampling_kernel(const int32_t* __restrict__ topk_ids, T* __restr
     is_finished[b] = out == end_id ? 1 : 0;
 }
 
+__global__ void sample_pick_kernel(const DecodeState* st, const int32_t* __restrict__ ids, float* __restrict__ v,
+                                   int K, uint64_t seed, unsigned long long* __restrict__ partials, int np) {
+    if (threadIdx.x == 0) {
+        const float mx = v[0];
+        float sum = 0.f;
+        for (int i = 0; i < K; ++i) {
+            v[i] = expf(v[i] - mx);
+            sum += v[i];
+        }
+        const uint64_t step = seed + (uint64_t)(st->cur_pos + 1);
+        const uint64_t r = prng::bits(prng::tensor_key(step, kSampleTid), 0ull);
+        float thr = (float)((r >> 40) + 1ull) * 0x1p-24f * sum;
+        int out = ids[0];
+        for (int i = 0; i < K; ++i) {
+            thr -= v[i];
+            if (thr <= 0.f) {
+                out = ids[i] % st->vocab;
+                break;
+            }
+        }
+        partials[0] = argmax_key(1.0f, (uint32_t)out);
+    }
+    for (int i = 1 + threadIdx.x; i < np; i += blockDim.x) partials[i] = 0ull;
+}
+
 template <typename T>
 int topk_dispatch(const void* logits, int rows, int vocab, int k, int32_t* ids, void* vals, hipStream_t s) {
     const T* x = static_cast<const T*>(logits);
@@ -143,6 +168,14 @@ int topk_dispatch(const void* logits, int rows, int vocab, int k, int32_t* ids, 
 }
 
 }  // namespace
+
+int sample_pick_launch(const DecodeState* st, const int32_t* ids, float* vals, int k, uint64_t seed,
+                       unsigned long long* partials, int np, hipStream_t s) {
+    LLMI_REQUIRE(st && ids && vals && partials && k >= 1 && k <= 16 && np >= 1, "sample_pick: bad arguments");
+    hipLaunchKernelGGL(sample_pick_kernel, dim3(1), dim3(256), 0, s, st, ids, vals, k, seed, partials, np);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
 
 int topk_launch(const void* logits, int dtype, int rows, int vocab, int k, int32_t* ids, void* vals, hipStream_t s) {
     LLMI_REQUIRE(logits && ids && vals && rows > 0 && vocab > 0, "topk: bad arguments");

@@ -73,6 +73,7 @@ _SIGS = {
     "llmi_engine_destroy": (_I, [_P]),
     "llmi_engine_load_synthetic": (_I, [_P, _U64]),
     "llmi_engine_load_bin": (_I, [_P, C.c_char_p]),
+    "llmi_engine_set_sampling": (_I, [_P, _I, _U64]),
     "llmi_engine_load_tensor": (_I, [_P, C.c_char_p, _P, _SZ]),
     "llmi_engine_set_prompt": (_I, [_P, _P, _I]),
     "llmi_engine_decode": (_I, [_P, _I, _I]),

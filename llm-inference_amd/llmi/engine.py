@@ -65,6 +65,10 @@ class Engine:
     def load_synthetic(self, seed: int):
         call("llmi_engine_load_synthetic", self._h, seed)
 
+    def set_sampling(self, k: int, seed: int = 0):
+        """Top-k stochastic sampling in the decode step (k = 0: greedy, the default)."""
+        call("llmi_engine_set_sampling", self._h, int(k), int(seed))
+
     def load_bin(self, weight_path: str):
         """Llama<T>::loadWeights(weight_path): weight_path + "<name>.bin" raw fp32 files
         (llmi/convert.py writes them); the path is used as a prefix, like the reference's."""
