@@ -33,6 +33,10 @@ public:
     LlamaModel& operator=(const LlamaModel&) = delete;
 
     void loadWeightsFromDummy(uint64_t seed = 0) { LLMI_CALL(llmi_engine_load_synthetic(eng, seed)); }
+    // Llama<T>::loadWeights(weight_path) (llama_weights.cc:41-53): weight_path + "<name>.bin", raw fp32
+    void loadWeights(const std::string& weight_path) { LLMI_CALL(llmi_engine_load_bin(eng, weight_path.c_str())); }
+    // Llama<T>::Sampling's top-k (llama.cpp:245-262) in the decode step; k = 0 (default) is greedy
+    void setSampling(int k, uint64_t seed = 0) { LLMI_CALL(llmi_engine_set_sampling(eng, k, seed)); }
 
     // Greedy generation (the reference's K = 1 top-k + sampling). tokens_per_sync
     // forwards run back to back (graph replays) between host reads, so the host
@@ -74,6 +78,16 @@ private:
     llmi_config cfg{};
     llmi_engine* eng = nullptr;
 };
+
+// model_utils.h:73-82 (CreateRealLLMModel): weights from the reference's .bin files (token ids in
+// and out: the tokenizer stays with the caller)
+inline std::unique_ptr<LlamaModel> CreateRealLLMModel(const std::string& weight_path,
+                                                      const std::string& preset = "llama2-7b",
+                                                      int weight_dtype = LLMI_F16) {
+    auto m = std::make_unique<LlamaModel>(preset, weight_dtype);
+    m->loadWeights(weight_path);
+    return m;
+}
 
 // model_utils.h:63-70
 inline std::unique_ptr<LlamaModel> CreateDummyLLMModel(const std::string& preset = "llama2-7b",
