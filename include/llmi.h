@@ -208,6 +208,7 @@ int llmi_synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint
  * kind: 0 host->device, 1 device->host, 2 device->device. */
 int llmi_device_alloc(void** ptr, size_t bytes);
 int llmi_device_free(void* ptr);
+int llmi_device_memset(void* ptr, int value, size_t bytes);
 int llmi_memcpy(void* dst, const void* src, size_t bytes, int kind);
 int llmi_device_sync(void);
 

@@ -31,8 +31,8 @@ public:
     virtual void UnifyFree(void* ptr, bool is_host) = 0;
 };
 
-// Plain device/host allocations (the reference's pooled CudaAllocator policy is out
-// of scope: the engine allocates every buffer once).
+// Plain device/host allocations; the reference's pooled CudaAllocator policy is
+// HipCachingAllocator (include/llmi/allocator.h). The engine allocates every buffer once.
 class HipAllocator : public BaseAllocator {
 public:
     void* UnifyMalloc(void* ptr, size_t size, bool is_host = false) override {

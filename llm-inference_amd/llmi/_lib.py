@@ -61,6 +61,7 @@ _SIGS = {
     "llmi_synth_fill_host": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I]),
     "llmi_synth_prompt": (_I, [_U64, _I, _I, _P]),
     "llmi_device_alloc": (_I, [C.POINTER(_P), _SZ]),
+    "llmi_device_memset": (_I, [_P, _I, _SZ]),
     "llmi_device_free": (_I, [_P]),
     "llmi_memcpy": (_I, [_P, _P, _SZ, _I]),
     "llmi_device_sync": (_I, []),
