@@ -304,9 +304,7 @@ int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes
 llmi_stream_t llmi_engine_stream(llmi_engine* e);
 /* Time `iters` eager launches of one kernel (HIP events on the engine stream);
  * launch i runs layer i % layers, so its weights stream from HBM as in decode.
- * which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head, 6 the whole layer as
- * the dataflow kernel (when the engine uses it; layer 0), 10..14 / 20..24 one
- * phase inside the dataflow kernel with / without its hand-off (diagnostics).
+ * which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head.
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
 /* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built
@@ -314,11 +312,6 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
  * workgroup at 8 * linear block id: start, two kernel-defined marks, end, CU id;
  * 100 MHz clock). NULL switches it off. */
 int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf);
-/* Debug timeline of one dataflow layer launch (layer 0): per workgroup, in
- * dispatch order, {start, wait passed, end} of the 100 MHz s_memrealtime clock
- * (3 x uint64 each, max_wg workgroups); phase_wgs[5] receives the workgroups of
- * the q/k/v, attention, o_proj, gate_up and down phases. */
-int llmi_engine_layer_stamps(llmi_engine* e, uint64_t* out, int max_wg, int* n_wg, int* phase_wgs);
 
 /* ---- In-process tensor-parallel group (no reference counterpart: the
  * reference has no TP). W rank engines with tp_rank 0..W-1 on ONE device and

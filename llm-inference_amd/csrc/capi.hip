@@ -181,7 +181,16 @@ int llmi_synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint
 
 int llmi_device_alloc(void** ptr, size_t bytes) {
     LLMI_REQUIRE(ptr != nullptr, "device_alloc: null out pointer");
-    LLMI_HIP(hipMalloc(ptr, bytes));
+    const hipError_t e = hipMalloc(ptr, bytes);
+    if (e != hipSuccess) {
+        // clear HIP's sticky last error: the caching allocator retries after releasing
+        // blocks, and the next launcher's hipGetLastError must not report this failure
+        (void)hipGetLastError();
+        *ptr = nullptr;
+        llmi::set_last_error(std::string("hipMalloc: ") + hipGetErrorString(e) + " (" + std::to_string(bytes) +
+                             " bytes)");
+        return LLMI_EHIP - (int)e;
+    }
     return LLMI_OK;
 }
 

@@ -93,14 +93,6 @@ struct Engine {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     ncclComm_t comm = nullptr;
-    // dataflow kernels (layer.hip): 0 none, 1 the whole layer as one launch (TP = 1),
-    // 2 attention + merge/o_proj as one launch (the latency-bound pair; any TP)
-    int fuse_mode = 0;
-    bool fused = false;            // fuse_mode == 1
-    int down_ksplit = 1;           // K-slices of the down projection (int64 atomic epilogue)
-    int grid_qkv = 0, grid_gu = 0, grid_down = 0;  // GEMV grid overrides (0: gemv_grid's choice)
-    int ring_grid_n = 0;           // ring layer grid (one workgroup per CU)
-    unsigned* layer_cnt = nullptr; // [layers][layer_cnt_words()] counters, zeroed by step_start
     // prefill scratch (allocated on first use): rows of one prefill chunk
     char* pf = nullptr;
     int pf_rows = 0;
@@ -254,8 +246,7 @@ struct Engine {
         const size_t o_par = take((size_t)lm_grid * 8);
         const size_t o_pr = take((size_t)c.max_seq * 4), o_tok = take((size_t)(c.max_seq + 1) * 4);
         const size_t o_rope = take((size_t)c.max_seq * c.head_dim * 4);
-        const size_t o_cnt = take((size_t)c.layers * layer_cnt_words() * 4);
-        LLMI_HIP(hipMalloc(&scratch, off));
+            LLMI_HIP(hipMalloc(&scratch, off));
         LLMI_HIP(hipMemsetAsync(scratch, 0, off, stream));
         attn_ws = scratch + o_ws;
         st = (DecodeState*)(scratch + o_st);
@@ -271,35 +262,6 @@ struct Engine {
         prompt = (int32_t*)(scratch + o_pr);
         tokens = (int32_t*)(scratch + o_tok);
         rope_tab = (float*)(scratch + o_rope);
-        layer_cnt = (unsigned*)(scratch + o_cnt);
-        {
-            const char* env = std::getenv("LLMI_FUSED");
-            // default (0): separate attention and merge/o_proj launches;
-            // LLMI_FUSED=1: whole dataflow layer (measured slower than five launches);
-            // LLMI_FUSED=2: dataflow attention + o_proj phases (measured even);
-            // LLMI_FUSED=3: attention + merge/o_proj co-scheduled per head in one launch
-            //               (attn.hip; measured 21.8 vs 19.8 us for the two launches at ctx 2048)
-            //               LLMI_FUSED=4: ring layer (ring.hip): attention merges in-kernel, then
-            //               o_proj + gate_up + down as one persistent launch with an LDS-DMA weight ring
-            //               LLMI_FUSED=5: attention merges in-kernel (last arriver), o_proj as a row GEMV
-            fuse_mode = !env ? 0 : (env[0] >= '1' && env[0] <= '5') ? env[0] - '0' : 0;
-            if (fuse_mode == 5 && (c.tp_world != 1 || grouped)) fuse_mode = 0;
-            if (fuse_mode == 4) {
-                ring_grid_n = ring_grid(device);
-                if (wdt != LLMI_F16 || c.tp_world != 1 || grouped || ring_check(ring_args(0), device) != LLMI_OK)
-                    fuse_mode = 0;
-            }
-            if (wdt == LLMI_F32 && (fuse_mode == 1 || fuse_mode == 2)) fuse_mode = 0;
-            if (fuse_mode == 1 && (c.tp_world != 1 || grouped)) fuse_mode = 2;
-            if (fuse_mode == 3 && attn_oproj_fused_check(attn_args_fused(0), o_args(0), device) != LLMI_OK)
-                fuse_mode = 0;  // shape unsupported or grid not co-resident: separate launches
-            fused = fuse_mode == 1;
-            const char* ks = std::getenv("LLMI_DOWN_KSPLIT");
-            down_ksplit = ks ? std::max(1, std::atoi(ks)) : (fused ? 4 : 1);
-            grid_qkv = env_int("LLMI_GRID_QKV");  // tuning overrides
-            grid_gu = env_int("LLMI_GRID_GU");
-            grid_down = env_int("LLMI_GRID_DOWN");
-        }
         // cos/sin cache with HF's fp32 arithmetic (LlamaRotaryEmbedding._set_cos_sin_cache):
         // inv_freq = 1 / fp32(base ** (2i/d)) (torch's fp32 pow is correctly rounded),
         // angle = fp32(pos * inv_freq), cos/sin correctly rounded to fp32
@@ -337,7 +299,7 @@ struct Engine {
             LLMI_TRY(fill(L.qkv, ql, lin, wdt, t(prng::K), kvrows, H, r * kvrows, 0, H));
             LLMI_TRY(fill(L.qkv, ql + kvrows, lin, wdt, t(prng::V), kvrows, H, r * kvrows, 0, H));
             // W_o row-major [H, ql] (a head-major layout measured no faster for the
-            // split-by-head o_proj, and the ring layer streams whole rows)
+            // split-by-head o_proj)
             LLMI_TRY(fill(L.o, 0, lin, wdt, t(prng::O), H, ql, 0, r * ql, c.heads * c.head_dim));
             // fused [gate; up] rows (layer_weights.cc:40 order)
             LLMI_TRY(fill(L.gu, 0, lin, wdt, t(prng::GATE), il, H, r * il, 0, H));
@@ -522,10 +484,6 @@ struct Engine {
         return a;
     }
 
-    static int env_int(const char* name) {
-        const char* e = std::getenv(name);
-        return e ? std::atoi(e) : 0;
-    }
     GemvArgs qkv_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
@@ -534,43 +492,6 @@ struct Engine {
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
-        a.grid = grid_qkv;
-        if (fuse_mode == 3 || fuse_mode == 5) {  // o_proj adds into xacc from its first workgroup on:
-            a.seed_src = res[l % 2]; a.seed_dst = xacc; a.seed_n = c.hidden;  // seed it here
-            a.seed_keep = c.tp_rank == 0 ? 1 : 0;                               // (rank 0 carries the residual)
-        }
-        return a;
-    }
-    AttnArgs attn_args_ring(int l) const {
-        AttnArgs a = attn_args(l);
-        a.xacc = nullptr;
-        a.merge_out = attn_out;  // merged per head in-kernel; the ring layer's o_proj input
-        return a;
-    }
-    GemvArgs o_gemv_args(int l) const {  // o_proj over whole rows of row-major W_o: xacc += W_o attn
-        const Layer& L = layers[l];
-        GemvArgs a;
-        a.stamps = dbg_stamps;
-        a.w = L.o; a.scales = L.o_s; a.w_dtype = wdt;
-        a.n_rows = c.hidden; a.k = ql; a.x = attn_out;
-        a.epi = EPI_ATOMIC; a.yacc = xacc; a.ksplit = 1;
-        return a;
-    }
-    RingArgs ring_args(int l) const {
-        const Layer& L = layers[l];
-        RingArgs a;
-        a.w_o = L.o; a.w_gu = L.gu; a.w_d = L.down; a.gamma = L.ffn_norm; a.eps = c.rms_eps;
-        a.hidden = c.hidden; a.q_dim = ql; a.inter = il;
-        a.attn = attn_out; a.resid = res[l % 2]; a.resid_keep = 1;
-        a.xmid = xacc; a.act = act; a.resid_out = res[(l + 1) % 2]; a.x_out = x;
-        a.cnt = layer_cnt + (size_t)l * layer_cnt_words();
-        a.err = &st->error;
-        a.stamps = dbg_stamps;
-        return a;
-    }
-    AttnArgs attn_args_fused(int l) const {
-        AttnArgs a = attn_args(l);
-        a.xacc = nullptr;  // seeded by the q/k/v GEMV instead
         return a;
     }
     AttnArgs attn_args(int l) const {
@@ -617,7 +538,6 @@ struct Engine {
         a.seed_keep = c.tp_rank == 0 ? 1 : 0;
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
-        a.grid = grid_gu;
         return a;
     }
     GemvArgs down_args(int l) const {
@@ -627,8 +547,7 @@ struct Engine {
         a.w = L.down; a.scales = L.down_s; a.w_dtype = wdt;
         a.n_rows = c.hidden; a.k = il; a.x = act;
         a.epi = EPI_ATOMIC; a.yacc = res[(l + 1) % 2];
-        a.ksplit = (il % (down_ksplit * (16 / (int)wsz))) == 0 ? down_ksplit : 1;
-        a.grid = grid_down ? grid_down * a.ksplit : 0;
+        a.ksplit = 1;
         return a;
     }
 
@@ -638,56 +557,19 @@ struct Engine {
     // group (struct Group) can interleave its ranks between the reductions.
     int rec_start() {
         return step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, res[0], c.max_seq,
-                                 (fuse_mode == 1 || fuse_mode == 2 || fuse_mode == 4) ? layer_cnt : nullptr, c.layers * layer_cnt_words(), stream);
-    }
-    LayerArgs layer_args(int l) const {
-        LayerArgs L;
-        L.qkv = qkv_args(l);
-        L.attn = attn_args(l);
-        L.o = o_args(l);
-        L.gu = gu_args(l);
-        L.down = down_args(l);
-        L.cnt = layer_cnt + (size_t)l * layer_cnt_words();
-        L.err = &st->error;
-        return L;
-    }
-    // one layer as the dataflow kernel; falls back to the five launches when the
-    // shape has no instantiation (and stays unfused from then on)
-    int rec_layer_fused(int l, bool* done) {
-        *done = false;
-        if (!fused) return LLMI_OK;
-        const int rc = layer_launch(layer_args(l), stream);
-        if (rc == LLMI_EUNSUPPORTED) {
-            fused = false;
-            return LLMI_OK;
-        }
-        LLMI_TRY(rc);
-        *done = true;
-        return LLMI_OK;
+                                 nullptr, 0, stream);
     }
     int rec_attn(int l) {
         LLMI_TRY(gemv_launch(qkv_args(l), stream));
-        if (fuse_mode == 3) return attn_oproj_fused_launch(attn_args_fused(l), o_args(l), &st->error, stream);
-        if (fuse_mode == 4) return attn_decode_launch(attn_args_ring(l), stream);
-        if (fuse_mode == 5) {  // merged attention, then o_proj as a row GEMV adding into xacc
-            LLMI_TRY(attn_decode_launch(attn_args_ring(l), stream));
-            return gemv_launch(o_gemv_args(l), stream);
-        }
-        if (fuse_mode == 2) {
-            const int rc = layer_launch_phases(layer_args(l), 1, 2, stream);
-            if (rc != LLMI_EUNSUPPORTED) return rc;
-            fuse_mode = 0;  // no instantiation for this shape: separate launches from now on
-        }
         LLMI_TRY(attn_decode_launch(attn_args(l), stream));
         return attn_oproj_launch(o_args(l), stream);
     }
     int rec_ffn(int l) {
-        if (fuse_mode == 4) return ring_layer_launch(ring_args(l), ring_grid_n, stream);
         LLMI_TRY(gemv_launch(gu_args(l), stream));
         return gemv_launch(down_args(l), stream);
     }
-    int rec_head() {
-        LLMI_TRY(gemv_launch(lm_args(), stream));
+    int rec_head(bool from_x = false) {
+        LLMI_TRY(gemv_launch(lm_args(from_x), stream));
         if (sample_k == 0) return LLMI_OK;
         // top-K of this token's logits, then the sampled id replaces the argmax partials
         LLMI_TRY(topk_launch(logits, LLMI_F32, 1, c.vocab, sample_k, samp_ids, samp_vals, stream));
@@ -702,6 +584,7 @@ struct Engine {
             LLMI_HIP(hipMalloc(&samp_vals, 16 * sizeof(float)));
         }
         if (exec) {  // the captured step changes: re-capture on the next graph decode
+            LLMI_HIP(hipStreamSynchronize(stream));  // a replay may still be in flight
             LLMI_HIP(hipGraphExecDestroy(exec));
             exec = nullptr;
         }
@@ -718,9 +601,6 @@ struct Engine {
         LLMI_REQUIRE(!grouped, "engine: a group rank is stepped by its group");
         LLMI_TRY(rec_start());
         for (int l = 0; l < c.layers; ++l) {
-            bool done = false;
-            LLMI_TRY(rec_layer_fused(l, &done));
-            if (done) continue;
             LLMI_TRY(rec_attn(l));
             if (comm) {  // exact int64 sum of the fixed-point residual partials
                 ncclResult_t r = ncclAllReduce(xacc, xacc, c.hidden, ncclInt64, ncclSum, comm, stream);
@@ -891,8 +771,7 @@ struct Engine {
             !gemm_supported(wdt, 2 * il, c.hidden, EPI_SILU_MUL) || !gemm_supported(wdt, c.hidden, il, EPI_ADD))
             return decode(n, 1);  // fp32 weights / odd shapes: the decode kernels, one row at a time
         LLMI_TRY(alloc_prefill());
-        const bool legacy = std::getenv("LLMI_PREFILL_LEGACY") != nullptr;  // A/B: register-staged GEMM
-        const bool use_gemm2 = !legacy && wdt == LLMI_F16 && gemm2_supported(ql + 2 * kvrows, c.hidden, EPI_STORE) &&
+        const bool use_gemm2 = wdt == LLMI_F16 && gemm2_supported(ql + 2 * kvrows, c.hidden, EPI_STORE) &&
                                gemm2_supported(c.hidden, ql, EPI_ADD) && gemm2_supported(2 * il, c.hidden, EPI_SILU_MUL) &&
                                gemm2_supported(c.hidden, il, EPI_ADD) && c.head_dim % 64 == 0;
         const int H = c.hidden, p_begin = host_next_pos;
@@ -941,12 +820,14 @@ struct Engine {
                 LLMI_TRY(gemm_launch(g, stream));
             }
             LLMI_TRY(prefill_flush(m));
-            if (p0 + m == p_begin + n) {  // last row -> final norm + lm_head + argmax keys
+            if (p0 + m == p_begin + n)  // last row -> x for the final norm + lm_head
                 LLMI_HIP(hipMemcpyAsync(x, pf_x + (size_t)(m - 1) * H, (size_t)H * 4, hipMemcpyDeviceToDevice, stream));
-                LLMI_TRY(gemv_launch(lm_args(true), stream));
-            }
         }
+        // the decode state first (cur_pos = last prompt row), then the head exactly as a
+        // decode step runs it -- lm_head + argmax keys, and the top-K draw at step
+        // seed + cur_pos + 1 when sampling (Llama<T>::firstTokenGen samples its token too)
         LLMI_TRY(prefill_finish_launch(st, prompt, tokens, p_begin, n, stream));
+        LLMI_TRY(rec_head(true));
         host_next_pos += n;
         return LLMI_OK;
     }
@@ -1265,37 +1146,6 @@ int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes
 
 llmi_stream_t llmi_engine_stream(llmi_engine* e) { return e ? (llmi_stream_t)e->e.stream : nullptr; }
 
-int llmi_engine_layer_stamps(llmi_engine* e, uint64_t* out, int max_wg, int* n_wg, int* phase_wgs) {
-    LLMI_REQUIRE(e && out && n_wg && phase_wgs, "layer_stamps: null argument");
-    Engine& g = e->e;
-    LLMI_HIP(hipSetDevice(g.device));
-    LLMI_REQUIRE(g.fused, "layer_stamps: the dataflow layer is not in use for this engine");
-    LLMI_REQUIRE(g.prompt_len > 0 && g.host_next_pos > 0, "layer_stamps: decode at least one step first");
-    llmi::LayerArgs L = g.layer_args(0);
-    const size_t cap = (size_t)max_wg * 3 * 8;
-    unsigned long long* dst = nullptr;
-    LLMI_HIP(hipMalloc(&dst, cap));
-    LLMI_HIP(hipMemsetAsync(dst, 0, cap, g.stream));
-    std::vector<char> save((size_t)g.c.hidden * 4);
-    LLMI_HIP(hipMemcpyAsync(save.data(), g.x, save.size(), hipMemcpyDeviceToHost, g.stream));
-    int rc = LLMI_OK;
-    for (int it = 0; it < 3 && rc == LLMI_OK; ++it) {  // the last of three launches is recorded
-        LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
-        L.stamps = (it == 2) ? dst : nullptr;
-        rc = llmi::layer_launch_probe(L, g.stream, max_wg, phase_wgs);
-    }
-    if (rc == LLMI_OK) {
-        LLMI_HIP(hipStreamSynchronize(g.stream));
-        int total = 0;
-        for (int p = 0; p < 5; ++p) total += phase_wgs[p];
-        *n_wg = total;
-        LLMI_HIP(hipMemcpy(out, dst, (size_t)std::min(total, max_wg) * 3 * 8, hipMemcpyDeviceToHost));
-    }
-    (void)hipFree(dst);
-    LLMI_HIP(hipMemcpy(g.x, save.data(), save.size(), hipMemcpyHostToDevice));
-    return rc;
-}
-
 int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf) {
     LLMI_REQUIRE(e, "debug_stamps: null engine");
     e->e.dbg_stamps = static_cast<unsigned long long*>(dev_buf);
@@ -1322,28 +1172,8 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             case 3: return llmi::gemv_launch(g.gu_args(l), g.stream);
             case 4: return llmi::gemv_launch(g.down_args(l), g.stream);
             case 5: return llmi::gemv_launch(g.lm_args(), g.stream);
-            case 7: return llmi::attn_oproj_fused_launch(g.attn_args_fused(l), g.o_args(l), &g.st->error, g.stream);
-            case 8: {  // ring layer (counters re-zeroed per launch)
-                LLMI_REQUIRE(g.ring_grid_n > 0, "time_kernel: the ring layer is not in use for this engine");
-                llmi::RingArgs ra = g.ring_args(l);
-                LLMI_HIP(hipMemsetAsync(ra.cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
-                return llmi::ring_layer_launch(ra, g.ring_grid_n, g.stream);
-            }
-            case 9: return llmi::attn_decode_launch(g.attn_args_ring(l), g.stream);
-            case 15: return llmi::gemv_launch(g.o_gemv_args(l), g.stream);
-            case 6: {  // dataflow layer 0 (counters re-zeroed per launch)
-                LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
-                return llmi::layer_launch(g.layer_args(0), g.stream);
-            }
-            case 10: case 11: case 12: case 13: case 14:    // one phase inside the dataflow kernel
-            case 20: case 21: case 22: case 23: case 24: {  // ... without the hand-off code
-                LLMI_HIP(hipMemsetAsync(g.layer_cnt, 0, (size_t)llmi::layer_cnt_words() * 4, g.stream));
-                llmi::LayerArgs L = g.layer_args(0);
-                L.plain_diag = which >= 20;
-                return llmi::layer_launch_phases(L, which % 10, which % 10, g.stream);
-            }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..9, 10..15 or 20..24");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..5");
     };
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
@@ -1355,37 +1185,10 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             b = (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb;
             break;
         }
-        case 2: case 15: b = (uint64_t)H * g.ql * ws + H * sc; break;
-        case 8: b = ((uint64_t)H * g.ql + 3ull * g.il * H) * ws + H * g.esz; break;
-        case 9: {
-            llmi::DecodeState hs;
-            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
-            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
-            b = (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb;
-            break;
-        }
-        case 7: {  // attention (K/V read + slot write) + W_o
-            llmi::DecodeState hs;
-            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
-            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
-            b = (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb +
-                (uint64_t)H * g.ql * ws + H * sc;
-            break;
-        }
+        case 2: b = (uint64_t)H * g.ql * ws + H * sc; break;
         case 3: b = (uint64_t)2 * g.il * H * ws + 2 * g.il * sc; break;
         case 4: b = (uint64_t)H * g.il * ws + H * sc; break;
         case 5: b = (uint64_t)g.vl * H * g.esz; break;
-        case 10: case 11: case 12: case 13: case 14:
-        case 20: case 21: case 22: case 23: case 24: b = 1; break;  // (bytes: see the standalone kernel)
-        case 6: {
-            LLMI_REQUIRE(g.fused, "time_kernel: the dataflow layer is not in use for this engine");
-            llmi::DecodeState hs;
-            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
-            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
-            b = (g.stream_bytes - (uint64_t)g.vl * H * g.esz - 2 * H * g.esz) / g.c.layers +
-                (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb;
-            break;
-        }
     }
     // timing launches modify the residual stream (o/down epilogues add into x),
     // so save and restore the small activation state around them

@@ -303,11 +303,6 @@ bool gemm2_supported(int n, int k, int epi) {
 
 int gemm2_bm(const Gemm2Args& a) {
     if (a.epi == EPI_SLAB) return 128;  // split-K supplies the workgroups
-    static const int forced = [] {
-        const char* e = std::getenv("LLMI_GEMM2_BM");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (forced == 64 || forced == 128) return forced;
     const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
     const int nt = ncols / ((a.epi == EPI_SILU_MUL) ? kBN / 2 : kBN);
     // 128-row tiles unless that leaves CUs idle

@@ -156,9 +156,6 @@ struct AttnArgs {
     const long long* resid_fixed = nullptr;
     float resid_scale = 1.f;
     int hidden = 0;
-    // engine (ring layer): the last-arriving split workgroup of each head merges the
-    // head's partials and writes merge_out[h * D .. +D] (fp32); xacc must be null
-    float* merge_out = nullptr;
 };
 
 // Merge of the split partials fused into the o_proj, split by head: workgroup
@@ -180,12 +177,6 @@ struct OprojArgs {
     long long* xacc = nullptr;
 };
 int attn_oproj_launch(const OprojArgs& a, hipStream_t s);
-// attention + merge/o_proj as one launch (attn.hip); aa.xacc must be null (the
-// residual seed moves to the q/k/v GEMV) and aa.direct_out 0. _check returns
-// LLMI_OK when the shape is supported and the whole grid is co-resident on `device`.
-int attn_oproj_fused_check(const AttnArgs& aa, const OprojArgs& oa, int device);
-int attn_oproj_fused_launch(const AttnArgs& aa, const OprojArgs& oa, int* err, hipStream_t s);
-
 // fixed-point residual accumulator: value = int64 * 2^-32
 __host__ __device__ __forceinline__ long long to_fixed(float v) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -200,58 +191,6 @@ __host__ __device__ __forceinline__ float from_fixed(long long v) {
 constexpr int kAttnChunk = 64;     // cached positions per workgroup (split-KV)
 size_t attn_workspace_bytes(int heads, int head_dim, int max_seq);
 int attn_decode_launch(const AttnArgs& a, hipStream_t s);
-
-// ------------------------------------------- ring layer (post-attention half)
-// o_proj + residual, RMSNorm + gate_up + SiLU*mul, down + residual as one
-// persistent launch with an LDS-DMA weight ring (ring.hip). fp16 weights,
-// row-major W_o [hidden, q_dim]; cnt: 2 * kPhaseCntWords u32, zero before launch.
-struct RingArgs {
-    const void* w_o = nullptr;
-    const void* w_gu = nullptr;     // [2 * inter, hidden] (gate rows, then up rows)
-    const void* w_d = nullptr;      // [hidden, inter]
-    const void* gamma = nullptr;    // ffn RMSNorm weight, fp16 [hidden]
-    float eps = 1e-5f;
-    int hidden = 0, q_dim = 0, inter = 0;
-    const float* attn = nullptr;    // merged attention output, fp32 [q_dim]
-    const long long* resid = nullptr;  // layer input residual (int64 fixed point)
-    int resid_keep = 1;
-    long long* xmid = nullptr;      // (unused: xmid is published in-launch as fp32 through x_out)
-    float* act = nullptr;           // silu(g) * u (published in-launch)
-    long long* resid_out = nullptr; // layer output residual
-    float* x_out = nullptr;         // fp32 xmid [hidden]: the in-launch all-gather buffer (= the engine's x)
-    unsigned* cnt = nullptr;
-    int* err = nullptr;
-    unsigned long long* stamps = nullptr;  // debug timeline (WgStamp + marks 5..7)
-};
-size_t ring_lds_bytes(const RingArgs& a);
-int ring_grid(int device);
-int ring_check(const RingArgs& a, int device);
-int ring_layer_launch(const RingArgs& a, int grid, hipStream_t s);
-
-// ------------------------------------------------ dataflow decode layer
-// One launch per layer: q/k/v GEMV, attention, merge + o_proj, gate_up, down
-// workgroups in phase order with counter hand-offs (layer.hip). nb/ns are set by
-// layer_launch; cnt (layer_cnt_words() u32) must be zero before each launch.
-struct LayerArgs {
-    GemvArgs qkv;
-    AttnArgs attn;
-    OprojArgs o;
-    GemvArgs gu;
-    GemvArgs down;
-    int nb[5] = {0, 0, 0, 0, 0};
-    int ns = 0;
-    unsigned* cnt = nullptr;
-    int* err = nullptr;            // sticky error word (DecodeState::error)
-    unsigned long long* stamps = nullptr;  // debug: 3 x u64 per workgroup (see layer.hip)
-    int plain_diag = 0;            // diagnostic: a one-phase launch without hand-off code
-};
-int layer_cnt_words();
-// LLMI_EUNSUPPORTED (nothing launched) when the shape/dtype has no instantiation
-int layer_launch(LayerArgs L, hipStream_t s);
-// same, reporting the per-phase workgroup counts (debug timelines)
-int layer_launch_probe(LayerArgs L, hipStream_t s, int max_wg, int* phase_wgs, int first = 0, int last = 4);
-// only phases first..last (0 q/k/v, 1 attention, 2 merge + o_proj, 3 gate_up, 4 down)
-int layer_launch_phases(LayerArgs L, int first, int last, hipStream_t s);
 
 // ------------------------------------------------------ decode-loop state
 struct DecodeState {

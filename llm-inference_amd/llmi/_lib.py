@@ -87,7 +87,6 @@ _SIGS = {
     "llmi_engine_bytes": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64)]),
     "llmi_engine_stream": (_P, [_P]),
     "llmi_engine_time_kernel": (_I, [_P, _I, _I, C.POINTER(_F), C.POINTER(_U64)]),
-    "llmi_engine_layer_stamps": (_I, [_P, _P, _I, C.POINTER(_I), _P]),
     "llmi_engine_debug_stamps": (_I, [_P, _P]),
     "llmi_group_create": (_I, [C.POINTER(Config), _I, _I, C.POINTER(_P)]),
     "llmi_group_destroy": (_I, [_P]),

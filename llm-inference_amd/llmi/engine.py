@@ -123,24 +123,12 @@ class Engine:
     def stream(self) -> int:
         return _lib.lib().llmi_engine_stream(self._h) or 0
 
-    KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5, "layer": 6, "attn_o": 7, "ring": 8, "attn_merge": 9, "o_gemv": 15,
-               "f_qkv": 10, "f_attn": 11, "f_o": 12, "f_gate_up": 13, "f_down": 14,
-               "p_qkv": 20, "p_attn": 21, "p_o": 22, "p_gate_up": 23, "p_down": 24}
+    KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5}
 
     def time_kernel(self, which: str, iters: int = 50):
         us, b = C.c_float(), C.c_uint64()
         call("llmi_engine_time_kernel", self._h, self.KERNELS[which], iters, C.byref(us), C.byref(b))
         return us.value, b.value
-
-    def layer_stamps(self, max_wg: int = 16384):
-        """Timeline of one dataflow layer launch: (stamps [n, 3] in us from the first
-        start, phase workgroup counts [5])."""
-        out = np.zeros((max_wg, 3), np.uint64)
-        n, ph = C.c_int(), np.zeros(5, np.int32)
-        call("llmi_engine_layer_stamps", self._h, out.ctypes.data, max_wg, C.byref(n), ph.ctypes.data)
-        st = out[:n.value].astype(np.int64)
-        st = (st - st[:, 0].min()) / 100.0  # 100 MHz ticks -> us
-        return st, ph
 
     def generate(self, prompt, n_new: int, use_graph: bool = True, prefill: bool = False,
                  exact: bool = True) -> np.ndarray:

@@ -180,27 +180,3 @@ def test_prefill_rejects_rows_past_prompt():
         e.set_prompt(np.arange(1, 9, dtype=np.int32))
         with pytest.raises(_lib.LlmiError, match="inside the prompt"):
             e.prefill(9)
-
-
-def test_prefill_gemm2_matches_legacy_gemm():
-    """The LDS-DMA GEMM path (gemm2.hip, fp16 planes) against the register-staged
-    GEMM path (gemm.hip) on the full 7B model: same tokens, logits within fp32
-    rounding of each other in the fp32-faithful mode."""
-    cfg = preset("llama2-7b", max_seq=256)
-    prompt = synth_prompt(1, 200, cfg.vocab)
-    out = {}
-    for legacy in (False, True):
-        if legacy:
-            os.environ["LLMI_PREFILL_LEGACY"] = "1"
-        try:
-            with Engine(cfg) as e:
-                e.load_synthetic(0)
-                e.set_prompt(prompt)
-                e.prefill(len(prompt), exact=True)
-                out[legacy] = (e.tokens()[: len(prompt) + 1], e.logits())
-        finally:
-            os.environ.pop("LLMI_PREFILL_LEGACY", None)
-    np.testing.assert_array_equal(out[False][0], out[True][0])
-    r = rel(out[False][1], out[True][1])
-    print(f"gemm2 vs legacy prefill logits rel-L2 {r:.2e}")
-    assert r < 1e-3  # 32 random-weight layers amplify rounding-order differences (north-star bar)
