@@ -253,7 +253,10 @@ int llmi_tp_comm_create(const void* tp_id, int world, int rank, int device, llmi
 int llmi_tp_allreduce(llmi_tp_comm* comm, void* buf, size_t count, int dtype, llmi_stream_t stream);
 int llmi_tp_comm_destroy(llmi_tp_comm* comm);
 
-/* device: HIP device ordinal. tp_id: 128-byte RCCL id or NULL when tp_world == 1. */
+/* device: HIP device ordinal. tp_id: 128-byte RCCL id (llmi_tp_unique_id, broadcast
+ * to every rank); required when tp_world > 1. With tp_world == 1 it may be NULL (no
+ * communicator) or an id: the engine then creates a one-rank communicator and runs
+ * the same RCCL all-reduces inside the token graph as a TP rank does (identities). */
 int llmi_engine_create(const llmi_config* cfg, int device, const void* tp_id, llmi_engine** out);
 int llmi_engine_destroy(llmi_engine* e);
 /* Llama<T>::loadWeightsFromDummy (src/models/llama/llama.h) with llmi-prng-v1 weights. */

@@ -161,7 +161,9 @@ struct Engine {
         } else {
             LLMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         }
-        if (W > 1 && !grouped) {
+        // a communicator whenever an id is given -- also at tp_world 1, where the
+        // all-reduces are identities but still run (captured in the token graph)
+        if (!grouped && (W > 1 || tp_id != nullptr)) {
             LLMI_REQUIRE(tp_id != nullptr, "engine: tp_world > 1 needs the RCCL unique id");
             ncclUniqueId id;
             std::memcpy(&id, tp_id, sizeof(id));

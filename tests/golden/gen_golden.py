@@ -16,11 +16,15 @@ as fp32, i.e. the reference's fp32 CPU path), and records inputs + outputs:
   f4_tp8.npz      f3 with pretraining_tp = 8 (sharded-linear semantics)
   f5_int8.npz     13B-width 1-layer W8A16 model (dequantised weights)
   f6_prefill.npz  7B-width 1 layer, prefill seq 512, last-token logits
+  f7_longctx.npz  2-layer 7B width, max_seq 2048: batched 2040-token prompt, then
+                  greedy steps to ctx 2048 (+ the oracle's fp16-KV emulation)
   tiny.npz        test_llama_run.py-like tiny model (hidden 512, 2 layers)
   manifest.json   versions + what each fixture holds
 
 Weights are NOT stored (they are regenerated from the seed); only ids,
-activations and outputs are. Usage: python tests/golden/gen_golden.py
+activations and outputs are. Usage: python tests/golden/gen_golden.py [f.npz ...]
+(all fixtures, or the named ones); --check regenerates everything into a temporary
+directory and compares the arrays with the committed fixtures.
 """
 from __future__ import annotations
 
@@ -209,7 +213,63 @@ def gen_f6(ref, seed=16, seq=512):
                         logits_rows=out.logits[0, [0, 1, 255, 511]].float().numpy())
 
 
-def main():
+@torch.no_grad()
+def gen_f7(ref, KV, seed=17, prompt_len=2040, n_new=9):
+    """The bench shape end to end at full context: 2 layers at 7B width, max_seq 2048.
+    The reference runs ONE batched forward over a 2040-token prompt (its cached path,
+    modeling_llama.py:351-454), then greedy steps until a forward at position 2047
+    (ctx 2048). Also recorded: the same run of the numpy oracle with an fp16 KV cache
+    (oracle/llama_ref.py, kv_dtype=float16), the emulation of the engine's throughput
+    mode, and each step's top-2 logit margin."""
+    from oracle.llama_ref import LlamaOracle
+    c = LlamaConfig(layers=2, max_seq=2048)
+    m = build_model(ref, c, seed)
+    prompt = prng.prompt_ids(seed, prompt_len, c.vocab)
+    t0 = time.perf_counter()
+    toks, first, last, kv = greedy_ref(ref, KV, m, prompt, n_new, keep_kv_pos=())
+    dt = time.perf_counter() - t0
+    o = LlamaOracle(c, seed=seed, kv_dtype=np.float16)
+    logits = o.prefill(prompt)
+    o_first, o_toks = logits.copy(), []
+    for i in range(n_new):
+        t = int(np.argmax(logits))
+        o_toks.append(t)
+        if i + 1 < n_new:
+            logits = o.forward_token(t)
+    np.savez_compressed(os.path.join(OUT, "f7_longctx.npz"), seed=seed, prompt=prompt, tokens=toks,
+                        first_logits=first, last_logits=last, ref_cpu_s=dt,
+                        f16kv_tokens=np.array(o_toks, np.int32), f16kv_first_logits=o_first,
+                        f16kv_last_logits=logits)
+    return toks
+
+
+def check():
+    """Regenerate every fixture into a temporary directory and compare its arrays with
+    the committed ones (timings excluded): the committed fixtures are what this script
+    produces from the reference (zip timestamps make a byte comparison meaningless)."""
+    global OUT
+    import tempfile
+    committed = OUT
+    with tempfile.TemporaryDirectory() as tmp:
+        OUT = tmp
+        main(write_manifest=False)
+        bad = []
+        for name in sorted(os.listdir(tmp)):
+            a = np.load(os.path.join(tmp, name), allow_pickle=False)
+            b = np.load(os.path.join(committed, name), allow_pickle=False)
+            keys = sorted(k for k in a.files if k != "ref_cpu_s")
+            if keys != sorted(k for k in b.files if k != "ref_cpu_s"):
+                bad.append(f"{name}: keys {keys} vs {sorted(b.files)}")
+                continue
+            for k in keys:
+                if not np.array_equal(a[k], b[k]):
+                    bad.append(f"{name}:{k}")
+        OUT = committed
+    print("fixtures reproduce" if not bad else "MISMATCH: " + ", ".join(bad))
+    return not bad
+
+
+def main(write_manifest=True):
     ref, KV = load_reference()
     torch.set_num_threads(os.cpu_count() or 8)
     import transformers
@@ -221,7 +281,8 @@ def main():
         ("f2_layer.npz", lambda: gen_f2(ref)),
         ("tiny.npz", lambda: gen_decode(ref, KV, LlamaConfig(hidden=512, heads=4, kv_heads=4,
                                                               inter=1024, layers=2, vocab=32000,
-                                                              max_seq=64), 21, 1, "tiny.npz", n_new=24)),
+                                                              max_seq=64), 21, 1, "tiny.npz", n_new=24,
+                                        keep_kv_pos=(0, 7, 23))),
         ("f3_decode.npz", lambda: gen_decode(ref, KV, LlamaConfig(layers=2), 13, 1, "f3_decode.npz")),
         ("f4_tp8.npz", lambda: gen_decode(ref, KV, LlamaConfig(layers=2), 13, 8, "f4_tp8.npz")),
         ("f5_int8.npz", lambda: gen_decode(ref, KV, LlamaConfig(hidden=5120, heads=40, kv_heads=40,
@@ -229,8 +290,9 @@ def main():
                                             "f5_int8.npz", n_new=8, int8=True,
                                             keep_kv_pos=(0, 7, 14))),
         ("f6_prefill.npz", lambda: gen_f6(ref)),
+        ("f7_longctx.npz", lambda: gen_f7(ref, KV)),
     ]
-    only = set(sys.argv[1:])
+    only = set(a for a in sys.argv[1:] if a.endswith(".npz"))
     for name, fn in steps:
         if only and name not in only:
             continue
@@ -238,6 +300,8 @@ def main():
         fn()
         print(f"{name}: {time.time() - t0:.1f}s", flush=True)
         manifest["fixtures"][name] = {"generated_s": round(time.time() - t0, 1)}
+    if not write_manifest:
+        return
     mpath = os.path.join(OUT, "manifest.json")
     if os.path.exists(mpath) and only:
         old = json.load(open(mpath))
@@ -247,4 +311,6 @@ def main():
 
 
 if __name__ == "__main__":
+    if "--check" in sys.argv:
+        sys.exit(0 if check() else 1)
     main()

@@ -127,3 +127,28 @@ def test_full_7b_decode_properties():
         assert len(set(t1.tolist())) > 1
         with pytest.raises(_lib.LlmiError, match="max_seq"):
             e.decode(1000)
+
+
+@pytest.mark.parametrize("kv_dtype,path", [(_lib.F32, "prefill"), (_lib.F32, "decode"),
+                                           (_lib.F16, "prefill"), (_lib.F16, "decode")])
+def test_7b_width_full_context_2048(kv_dtype, path):
+    """The bench shape at full context (f7_longctx.npz): 2 layers at 7B width, max_seq
+    2048, a 2040-token prompt -- prefilled in chunks of 512 rows, or fed token by token
+    through the decode graph -- then greedy steps whose last forward runs at position
+    2047 (ctx 2048, 32 split-KV chunks). fp32 KV against the reference's own run;
+    fp16 KV (the bench's cache) against the oracle with the same cache rounding."""
+    f = load("f7_longctx.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=2048)
+    cfg.kv_dtype = kv_dtype
+    n = len(f["tokens"])
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        toks = e.generate(f["prompt"], n, prefill=(path == "prefill"))
+        logits = e.logits()
+    exp_t, exp_l = (f["tokens"], f["last_logits"]) if kv_dtype == _lib.F32 else \
+        (f["f16kv_tokens"], f["f16kv_last_logits"])
+    np.testing.assert_array_equal(toks, exp_t)
+    r = rel(logits, exp_l)
+    print(f"f7 ctx 2048 kv={'f32' if kv_dtype == _lib.F32 else 'f16'} {path}: logits rel-L2 {r:.3e} "
+          f"(vs reference fp32: {rel(logits, f['last_logits']):.3e})")
+    assert r < LOGIT_TOL

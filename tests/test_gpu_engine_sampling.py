@@ -19,7 +19,7 @@ def _fixture():
     return np.load(os.path.join(REPO, "tests", "golden", "tiny.npz"), allow_pickle=False)
 
 
-def _engine_tokens(k, seed, n, use_graph=True):
+def _engine_tokens(k, seed, n, use_graph=True, prefill=False):
     import llmi
     from llmi.engine import Engine, preset
     f = _fixture()
@@ -28,7 +28,7 @@ def _engine_tokens(k, seed, n, use_graph=True):
     with Engine(cfg) as e:
         e.load_synthetic(int(f["seed"]))
         e.set_sampling(k, seed)
-        return e.generate(f["prompt"], n, use_graph=use_graph)
+        return e.generate(f["prompt"], n, use_graph=use_graph, prefill=prefill)
 
 
 def _oracle_tokens(k, seed, n):
@@ -70,3 +70,12 @@ def test_engine_sampling_argument_checks():
     with Engine(preset("tiny")) as e:
         with pytest.raises(LlmiError, match="k must be"):
             e.set_sampling(17, 0)
+
+
+@pytest.mark.parametrize("k,seed", [(5, 11), (16, 12345)])
+def test_engine_sampling_after_prefill_matches_decode_path(k, seed):
+    """firstTokenGen samples too: the token after a batched prefill is drawn at step
+    seed + prompt_len, exactly as the token-by-token path draws it."""
+    got = _engine_tokens(k, seed, 10, prefill=True)
+    np.testing.assert_array_equal(got, _engine_tokens(k, seed, 10))
+    np.testing.assert_array_equal(got, _oracle_tokens(k, seed, 10))

@@ -102,3 +102,21 @@ def test_prng_shard_slices_match_full():
     full = prng.linear_fp16(3, 0x105, 16, 32)
     part = prng.linear_fp16(3, 0x105, 8, 8, row0=4, col0=16, ld=32)
     np.testing.assert_array_equal(full[4:12, 16:24], part)
+
+
+@pytest.mark.slow
+def test_f7_longctx_prefill_2040_then_decode_to_ctx_2048():
+    """The oracle's batched prefill over a 2040-token prompt and its decode steps to
+    ctx 2048 against the reference's own run (f7_longctx.npz)."""
+    f = load("f7_longctx.npz")
+    o = R.LlamaOracle(R.LlamaConfig(layers=2, max_seq=2048), seed=int(f["seed"]))
+    logits = o.prefill(f["prompt"])
+    assert rel_l2(logits, f["first_logits"]) < 1e-5
+    toks = []
+    for i in range(len(f["tokens"])):
+        toks.append(int(np.argmax(logits)))
+        if i + 1 < len(f["tokens"]):
+            logits = o.forward_token(toks[-1])
+    np.testing.assert_array_equal(toks, f["tokens"])
+    assert o.pos == 2048  # the last forward ran at position 2047
+    assert rel_l2(logits, f["last_logits"]) < 1e-5
