@@ -836,7 +836,7 @@ struct Engine {
 
     int tokens_out(int32_t* out, int n, int* n_valid) {
         int valid = host_next_pos;
-        if (host_next_pos >= prompt_len && host_next_pos < c.max_seq) {
+        if (host_next_pos >= prompt_len && host_next_pos <= c.max_seq) {
             LLMI_TRY(finalize_launch(st, partials, lm_grid, tokens, c.max_seq, stream));
             valid = host_next_pos + 1;
         }

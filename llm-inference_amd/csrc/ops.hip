@@ -189,7 +189,8 @@ __global__ void finalize_kernel(DecodeState* st, const unsigned long long* parti
     unsigned long long best = 0;
     for (int i = threadIdx.x; i < np; i += blockDim.x) best = partials[i] > best ? partials[i] : best;
     best = block_max_key(best, sh);
-    if (threadIdx.x == 0 && p < max_seq && p >= st->prompt_len) tokens[p] = (int)argmax_key_index(best);
+    // tokens holds max_seq + 1 ids: the token chosen by the forward at position max_seq - 1 too
+    if (threadIdx.x == 0 && p <= max_seq && p >= st->prompt_len) tokens[p] = (int)argmax_key_index(best);
 }
 
 // ------------------------------------------------------ synthetic weights
