@@ -302,6 +302,18 @@ def main(write_manifest=True):
         manifest["fixtures"][name] = {"generated_s": round(time.time() - t0, 1)}
     if not write_manifest:
         return
+    # data fixture copied from the reference (not generated): the tokenizer vocabulary
+    import hashlib
+    import shutil
+    tok_src = os.path.join(os.path.dirname(REF), "llama2-7b-tokenizer.bin")
+    tok_dst = os.path.join(OUT, "llama2-7b-tokenizer.bin")
+    shutil.copyfile(tok_src, tok_dst)
+    manifest["fixtures"]["llama2-7b-tokenizer.bin"] = {
+        "source": "copied verbatim from /root/reference/llama2-7b-tokenizer.bin (data file the reference's "
+                  "user_entry.cpp:8 loads)",
+        "sha256": hashlib.sha256(open(tok_dst, "rb").read()).hexdigest(),
+        "known_answer": "src/models/llama/llama.cpp:382 hard-coded ids of 'Hey, are you conscious? Can you "
+                        "talk to me?'"}
     mpath = os.path.join(OUT, "manifest.json")
     if os.path.exists(mpath) and only:
         old = json.load(open(mpath))
