@@ -179,9 +179,9 @@ void launchSampling(TensorWrapper<int>* topk_id, TensorWrapper<T>* topk_val, Ten
 // q [batch, heads, seq, head], k, v [batch, kv_heads, seq, head], RoPE at history + s.
 // Llama has no qkv bias (qkv.bias is ignored); v is written (the reference leaves it
 // unset) and positions are per sequence (include/llmi.h: llmi_rope_qkv_prefill).
-template <typename T>
+template <typename T, typename WT>
 void launchAddFusedQKVBiasTransposeAndRoPE(TensorWrapper<T>* q_buf, TensorWrapper<T>* k_buf, TensorWrapper<T>* v_buf,
-                                           TensorWrapper<T>* QKV, BaseWeight<T>& qkv,
+                                           TensorWrapper<T>* QKV, BaseWeight<WT>& qkv,
                                            TensorWrapper<int>* padding_offset, TensorWrapper<int>* history_length,
                                            TensorWrapper<int>* input_length, LLaMAAttentionStaticParams& params,
                                            void* stream = nullptr) {

@@ -4,6 +4,8 @@
 //   LLaMASelfAttentionLayer<T>::Forward  src/layers/attention/masked_self_attention.h:53
 //   LLaMAFFNLayer<T>::forward            src/layers/ffn/ffn.h:50
 //   LlamaSelfDecoder<T>::forward         src/layers/decoder/self_decoder.h:65
+//   LLaMAContextAttentionLayer<T>::forward src/layers/attention/context_attention.h:60
+//   LlamaContextDecoder<T>::forward      src/layers/decoder/context_decoder.h:74
 // Same TensorMap keys ("attention_input", "attention_output", "all_k_cache",
 // "all_v_cache", "step", "layer_id", "finished", "ffn_input", "ffn_output",
 // "decoder_input", "decoder_output") and the same per-layer dataflow
@@ -14,6 +16,7 @@
 // (#13), layer_id is a valid host tensor per layer (#14), decode FFN scratch is
 // one token (#15), the down weight is [H, I] (#21).
 #pragma once
+#include <cmath>
 #include <cstdlib>
 #include <memory>
 #include <vector>
@@ -140,10 +143,25 @@ public:
         mha_output.reset();
     }
 
-    // masked_self_attention.cpp:54-92: qkv GEMV -> RoPE -> fused KV write + MHA -> o_proj
-    template <typename CT>
+    // masked_self_attention.cpp:54-92: qkv GEMV -> RoPE -> fused KV write + MHA -> o_proj.
+    // The reference's call (self_decoder.cpp:64): the cache element type comes from the
+    // "all_k_cache" tensor's dtype at run time (FP32 for parity, FP16 for throughput).
     void Forward(TensorMap& inputs, TensorMap& outputs, LLaMAattentionWeights<T>& weights,
                  LLaMAAttentionDynParams& params) {
+        const DataType cdt = outputs["all_k_cache"]->dtype;
+        LLM_CHECK_WITH_INFO(outputs["all_v_cache"]->dtype == cdt, "k and v caches must have the same dtype");
+        if (cdt == FP32)
+            ForwardCache<float>(inputs, outputs, weights, params);
+        else if (cdt == FP16)
+            ForwardCache<half_t>(inputs, outputs, weights, params);
+        else
+            LLM_CHECK_WITH_INFO(false, "kv cache dtype must be FP32 or FP16");
+    }
+
+private:
+    template <typename CT>
+    void ForwardCache(TensorMap& inputs, TensorMap& outputs, LLaMAattentionWeights<T>& weights,
+                      LLaMAAttentionDynParams& params) {
         allocForForward(params);
         TensorWrapper<float>* attention_input = inputs["attention_input"]->as<float>();
         TensorWrapper<float>* attention_output = outputs["attention_output"]->as<float>();
@@ -161,7 +179,6 @@ public:
                          false, true);
     }
 
-private:
     int head_num, kv_head_num, head_size, hidden;
     LLaMAAttentionStaticParams attn_static_params;
     void* stream;
@@ -180,23 +197,28 @@ public:
         : inter_size(inter_size), hidden(head_num * head_size), stream(stream), cublas_wrapper(cublas_wrapper),
           allocator(allocator) {}
     ~LLaMAFFNLayer() { freeBuf(); }
-    void allocForForward(int batch_size) {
-        if (SwiGLU_input) return;
-        gu_ptr = allocator->Malloc(gu_ptr, sizeof(float) * batch_size * 2 * inter_size, false);
-        act_ptr = allocator->Malloc(act_ptr, sizeof(float) * batch_size * inter_size, false);
-        SwiGLU_input = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{batch_size, 2, inter_size}, gu_ptr);
-        down_proj_input = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{batch_size, inter_size}, act_ptr);
+    // rows: batch_size in decode, num_tokens in the context phase (ffn.cpp:55-60)
+    void allocForForward(int rows) {
+        if (rows > cap) {
+            freeBuf();
+            gu_ptr = allocator->Malloc(gu_ptr, sizeof(float) * rows * 2 * inter_size, false);
+            act_ptr = allocator->Malloc(act_ptr, sizeof(float) * rows * inter_size, false);
+            cap = rows;
+        }
+        SwiGLU_input = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{rows, 2, inter_size}, gu_ptr);
+        down_proj_input = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{rows, inter_size}, act_ptr);
     }
     void freeBuf() {
         if (gu_ptr) allocator->Free(gu_ptr, false);
         if (act_ptr) allocator->Free(act_ptr, false);
         gu_ptr = act_ptr = nullptr;
+        cap = 0;
         SwiGLU_input.reset();
         down_proj_input.reset();
     }
     // ffn.cpp:52-93: gate_up GEMV -> SiLU*mul -> down GEMV
     void forward(TensorMap& inputs, TensorMap& outputs, LLaMAFFNWeights<T>& weights, LLaMAAttentionDynParams& params) {
-        allocForForward(params.batch_size);
+        allocForForward(params.is_ctx ? params.num_tokens : params.batch_size);
         TensorWrapper<float>* ffn_input = inputs["ffn_input"]->as<float>();
         TensorWrapper<float>* ffn_output = outputs["ffn_output"]->as<float>();
         cublasWrapper cw{stream};
@@ -212,6 +234,7 @@ private:
     cublasWrapper* cublas_wrapper;
     BaseAllocator* allocator;
     float *gu_ptr = nullptr, *act_ptr = nullptr;
+    int cap = 0;
     std::unique_ptr<TensorWrapper<float>> SwiGLU_input, down_proj_input;
 };
 
@@ -231,14 +254,15 @@ public:
     }
 
     // self_decoder.cpp:23-89 for one token; inputs "decoder_input" [1, H], "step" and
-    // "layer_id" (host int), "finished"; outputs "decoder_output", "all_k_cache", "all_v_cache".
-    template <typename CT>
+    // "layer_id" (host int), "finished"; outputs "decoder_output", "all_k_cache", "all_v_cache"
+    // (FP32 or FP16 caches, chosen by their dtype).
     void forward(TensorMap& input_tensors, const std::vector<LlamaLayerWeight<T>*>& layerWeights,
                  TensorMap& output_tensors, LLaMAAttentionDynParams& dyn_params) {
         if (!resid_ptr) {
             resid_ptr = allocator->Malloc(resid_ptr, sizeof(float) * dyn_params.batch_size * hidden, false);
             decoder_residual = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{dyn_params.batch_size, hidden}, resid_ptr);
         }
+        dyn_params.is_ctx = false;  // one token: FFN scratch is batch_size rows
         TensorWrapper<float>* decoder_input = input_tensors["decoder_input"]->as<float>();
         TensorWrapper<float>* decoder_output = output_tensors["decoder_output"]->as<float>();
         int layer = 0;
@@ -252,7 +276,7 @@ public:
             LlamaLayerWeight<T>* w = layerWeights[layer];
             // decoder_input <- RMSNorm(x), residual <- x
             launchRMSNorm(decoder_input, decoder_residual.get(), w->attn_norm_weight, rmsnorm_eps, false, stream);
-            selfAttn.template Forward<CT>(attn_in, attn_out, w->self_attn_weight, dyn_params);
+            selfAttn.Forward(attn_in, attn_out, w->self_attn_weight, dyn_params);
             // residual += attention_out; decoder_output <- RMSNorm(residual)
             BaseWeight<T> no_bias;
             launchFusedAddBiasResidualRMSNorm(decoder_residual.get(), decoder_output, no_bias, w->ffn_norm_weight.gamma,
@@ -273,4 +297,189 @@ private:
     LLaMAFFNLayer<T> ffn;
     float* resid_ptr = nullptr;
     std::unique_ptr<TensorWrapper<float>> decoder_residual;
+};
+
+// ------------------------------------------------------ context phase
+// LLaMAContextAttentionLayer<T>::forward (context_attention.cpp:85-174) over the
+// context launchers: qkv GEMM -> RoPE + transpose (with history offsets) -> KV
+// concat -> repeat_kv -> QK^T -> scale + causal mask + softmax -> PV -> transpose +
+// remove padding -> o_proj. Activations and caches fp32 (the reference's working
+// Llama<float>); the engine's fused MFMA prefill (llmi_engine_prefill) is the fast
+// path. Fixed relative to the reference: the qkv buffer holds all
+// (heads + 2 kv) heads and QK^T uses the repeated cache (history included), not the
+// current query's un-repeated k.
+template <typename T>
+class LLaMAContextAttentionLayer {
+public:
+    LLaMAContextAttentionLayer(int head_num, int kv_head_num, int head_size, LLaMAAttentionStaticParams attn_params,
+                               void* stream, cublasWrapper* cublas_wrapper, BaseAllocator* allocator)
+        : head_num(head_num), kv_head_num(kv_head_num), head_size(head_size), hidden_units(head_num * head_size),
+          q_head_per_kv(head_num / kv_head_num), scale(1.0f / std::sqrt((float)head_size)),
+          attn_static_params(attn_params), stream(stream), cublas_wrapper(cublas_wrapper), allocator(allocator) {}
+    ~LLaMAContextAttentionLayer() { freeBuf(); }
+    LLaMAAttentionStaticParams& GetAttnStaticParams() { return attn_static_params; }
+
+    // context_attention.cpp:26-74: buffers sized by batch_size, num_tokens, max_q_len, max_k_len
+    void allocForForward(LLaMAAttentionDynParams& p) {
+        freeBuf();
+        const int qkv_heads = head_num + 2 * kv_head_num, b = p.batch_size, q = p.max_q_len, k = p.max_k_len;
+        qkv_buf_wo_pad = make({p.num_tokens, qkv_heads, head_size});
+        q_buf_w_pad = make({b, head_num, q, head_size});
+        k_buf_w_pad = make({b, kv_head_num, q, head_size});
+        v_buf_w_pad = make({b, kv_head_num, q, head_size});
+        k_cache_buf = make({b, head_num, k, head_size});
+        v_cache_buf = make({b, head_num, k, head_size});
+        qk_buf = make({b, head_num, q, k});
+        qkv_buf_w_pad = make({b, head_num, q, head_size});
+        qkv_buf_wo_pad_1 = make({p.num_tokens, head_num, head_size});
+    }
+    void freeBuf() {
+        for (auto& t : bufs) allocator->Free(t->data, false);
+        bufs.clear();
+    }
+
+    // inputs: "attention_input" [num_tokens, H], "padding_offset", "history_length",
+    // "input_length", "context_length" (device int), "layer_id" (host int),
+    // "attention_mask" [bs, max_q_len, max_k_len]; outputs: "attention_output"
+    // [num_tokens, H], "all_k_cache" / "all_v_cache" [layers, bs, kv_heads, max_seq, head]
+    void forward(TensorMap& inputs, TensorMap& outputs, LLaMAattentionWeights<T>& weights,
+                 LLaMAAttentionDynParams& params, LLaMAAttentionStaticParams& static_params) {
+        LLM_CHECK_WITH_INFO(outputs["all_k_cache"]->dtype == FP32,
+                            "the context attention layer keeps an fp32 cache (the engine's prefill handles fp16)");
+        allocForForward(params);
+        cublasWrapper cw{stream};
+        cublasWrapper* c = cublas_wrapper ? cublas_wrapper : &cw;
+        TensorWrapper<int>* padding_offset = inputs["padding_offset"]->as<int>();
+        TensorWrapper<int>* history_length = inputs["history_length"]->as<int>();
+        TensorWrapper<int>* input_length = inputs["input_length"]->as<int>();
+        TensorWrapper<int>* context_length = inputs["context_length"]->as<int>();
+        TensorWrapper<int>* layer_id = inputs["layer_id"]->as<int>();
+        TensorWrapper<float>* all_k_cache = outputs["all_k_cache"]->as<float>();
+        TensorWrapper<float>* all_v_cache = outputs["all_v_cache"]->as<float>();
+        // 1. qkv linear
+        launchLinearGemm(inputs["attention_input"]->as<float>(), weights.qkv, qkv_buf_wo_pad, c, false, true);
+        // 2. RoPE (position history + s) and [num_tokens, ...] -> [bs, heads, max_q_len, head]
+        launchAddFusedQKVBiasTransposeAndRoPE(q_buf_w_pad, k_buf_w_pad, v_buf_w_pad, qkv_buf_wo_pad, weights.qkv,
+                                              padding_offset, history_length, input_length, static_params, stream);
+        // 3. append this prompt's k, v to the layer's cache after the history
+        launchConcatKVCache(k_buf_w_pad, v_buf_w_pad, layer_id, input_length, history_length, all_k_cache,
+                            all_v_cache, stream);
+        // 4. history + prompt, kv heads repeated to the query heads
+        launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, k_cache_buf, v_cache_buf, stream);
+        launchLinearStridedBatchGemm(q_buf_w_pad, k_cache_buf, qk_buf, c, false, true);
+        launchScaleMaskAndSoftmax(qk_buf, inputs["attention_mask"]->as<float>(), qk_buf, scale, stream);
+        launchLinearStridedBatchGemm(qk_buf, v_cache_buf, qkv_buf_w_pad, c, false, false);
+        // 5. [bs, heads, max_q_len, head] -> [num_tokens, H], then o_proj
+        launchTransposeOutRemovePadding(qkv_buf_w_pad, padding_offset, qkv_buf_wo_pad_1, stream);
+        launchLinearGemm(qkv_buf_wo_pad_1, weights.output, outputs["attention_output"]->as<float>(), c, false, true);
+        freeBuf();
+    }
+
+private:
+    TensorWrapper<float>* make(std::vector<int> shape) {
+        size_t n = 1;
+        for (int d : shape) n *= (size_t)d;
+        float* p = nullptr;
+        p = allocator->Malloc(p, sizeof(float) * n, false);
+        bufs.push_back(std::make_unique<TensorWrapper<float>>(GPU, FP32, shape, p));
+        return bufs.back().get();
+    }
+    int head_num, kv_head_num, head_size, hidden_units, q_head_per_kv;
+    float scale;
+    LLaMAAttentionStaticParams attn_static_params;
+    void* stream;
+    cublasWrapper* cublas_wrapper;
+    BaseAllocator* allocator;
+    std::vector<std::unique_ptr<TensorWrapper<float>>> bufs;
+    TensorWrapper<float> *qkv_buf_wo_pad = nullptr, *q_buf_w_pad = nullptr, *k_buf_w_pad = nullptr,
+                         *v_buf_w_pad = nullptr, *k_cache_buf = nullptr, *v_cache_buf = nullptr, *qk_buf = nullptr,
+                         *qkv_buf_w_pad = nullptr, *qkv_buf_wo_pad_1 = nullptr;
+};
+
+// LlamaContextDecoder<T>::forward (context_decoder.cpp:47-143): padding offsets and
+// the causal mask once, then per layer RMSNorm -> context attention -> fused
+// residual + RMSNorm -> FFN (num_tokens rows) -> residual.
+// inputs: "decoder_input" [num_tokens, H] (embedded prompt rows, overwritten),
+// "history_length", "input_length", "context_length" (device int [bs]),
+// "layer_id" (host int); outputs: "decoder_output" [num_tokens, H], "all_k_cache",
+// "all_v_cache" (fp32). dyn_params: batch_size, num_tokens, max_q_len, max_k_len.
+template <typename T>
+class LlamaContextDecoder {
+public:
+    LlamaContextDecoder(int head_num, int kv_head_num, int head_size, int inter_size, int num_layer,
+                        const LLaMAAttentionStaticParams& attn_params, float rmsnorm_eps, void* stream,
+                        cublasWrapper* cublas_wrapper, BaseAllocator* allocator)
+        : hidden_units(head_num * head_size), num_layer(num_layer), rmsnorm_eps(rmsnorm_eps), stream(stream),
+          allocator(allocator),
+          ctxAttn(head_num, kv_head_num, head_size, attn_params, stream, cublas_wrapper, allocator),
+          ffn(head_num, head_size, inter_size, stream, cublas_wrapper, allocator) {}
+    ~LlamaContextDecoder() { freeBuf(); }
+
+    void allocForForward(LLaMAAttentionDynParams& p) {
+        freeBuf();
+        mask_ptr = allocator->Malloc(mask_ptr, sizeof(float) * p.batch_size * p.max_q_len * p.max_k_len, false);
+        po_ptr = allocator->Malloc(po_ptr, sizeof(int) * p.batch_size * p.max_q_len, false);
+        cum_ptr = allocator->Malloc(cum_ptr, sizeof(int) * (p.batch_size + 1), false);
+        resid_ptr = allocator->Malloc(resid_ptr, sizeof(float) * p.num_tokens * hidden_units, false);
+        attention_mask = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{p.batch_size, p.max_q_len, p.max_k_len}, mask_ptr);
+        padding_offset = std::make_unique<TensorWrapper<int>>(GPU, INT32, std::vector<int>{p.batch_size, p.max_q_len}, po_ptr);
+        cum_seqlens = std::make_unique<TensorWrapper<int>>(GPU, INT32, std::vector<int>{p.batch_size + 1}, cum_ptr);
+        decoder_residual = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{p.num_tokens, hidden_units}, resid_ptr);
+    }
+    void freeBuf() {
+        for (void* p : {(void*)mask_ptr, (void*)po_ptr, (void*)cum_ptr, (void*)resid_ptr})
+            if (p) allocator->UnifyFree(p, false);
+        mask_ptr = resid_ptr = nullptr;
+        po_ptr = cum_ptr = nullptr;
+    }
+
+    void forward(TensorMap& input_tensors, const std::vector<LlamaLayerWeight<T>*>& layerWeights,
+                 TensorMap& output_tensors, LLaMAAttentionDynParams& dyn_params) {
+        allocForForward(dyn_params);
+        Tensor* seq_lens = input_tensors["input_length"];
+        launchCalPaddingoffset(padding_offset.get(), cum_seqlens.get(), seq_lens->as<int>(), stream);
+        launchBuildCausalMasks(attention_mask.get(), seq_lens->as<int>(), input_tensors["context_length"]->as<int>(),
+                               stream);
+        TensorWrapper<float>* decoder_output = output_tensors["decoder_output"]->as<float>();
+        int layer = 0;
+        TensorWrapper<int> layer_id(CPU, INT32, {1}, &layer);
+        TensorMap ctx_attn_inputs{{"attention_input", input_tensors["decoder_input"]},
+                                  {"padding_offset", padding_offset.get()},
+                                  {"history_length", input_tensors["history_length"]},
+                                  {"input_length", seq_lens},
+                                  {"layer_id", &layer_id},
+                                  {"context_length", input_tensors["context_length"]},
+                                  {"attention_mask", attention_mask.get()}};
+        TensorMap ctx_attn_output{{"attention_output", decoder_output},
+                                  {"all_k_cache", output_tensors["all_k_cache"]},
+                                  {"all_v_cache", output_tensors["all_v_cache"]}};
+        TensorMap ffn_inputs{{"ffn_input", decoder_output}}, ffn_outputs{{"ffn_output", decoder_output}};
+        dyn_params.is_ctx = true;  // FFN scratch of num_tokens rows
+        for (layer = 0; layer < num_layer; ++layer) {
+            LlamaLayerWeight<T>* w = layerWeights[layer];
+            TensorWrapper<float>* decoder_input = ctx_attn_inputs["attention_input"]->as<float>();
+            launchRMSNorm(decoder_input, decoder_residual.get(), w->attn_norm_weight, rmsnorm_eps, false, stream);
+            ctxAttn.forward(ctx_attn_inputs, ctx_attn_output, w->self_attn_weight, dyn_params,
+                            ctxAttn.GetAttnStaticParams());
+            BaseWeight<T> no_bias;  // Llama has no o_proj bias (the reference passed the weight itself)
+            launchFusedAddBiasResidualRMSNorm(decoder_residual.get(), decoder_output, no_bias, w->ffn_norm_weight.gamma,
+                                              rmsnorm_eps, stream);
+            ffn.forward(ffn_inputs, ffn_outputs, w->ffn_weight, dyn_params);
+            launchAddResidual(decoder_residual.get(), decoder_output, false, stream);
+            ctx_attn_inputs.insert("attention_input", decoder_output);
+        }
+        freeBuf();
+    }
+
+private:
+    int hidden_units, num_layer;
+    float rmsnorm_eps;
+    void* stream;
+    BaseAllocator* allocator;
+    LLaMAContextAttentionLayer<T> ctxAttn;
+    LLaMAFFNLayer<T> ffn;
+    float *mask_ptr = nullptr, *resid_ptr = nullptr;
+    int *po_ptr = nullptr, *cum_ptr = nullptr;
+    std::unique_ptr<TensorWrapper<float>> attention_mask, decoder_residual;
+    std::unique_ptr<TensorWrapper<int>> padding_offset, cum_seqlens;
 };

@@ -145,7 +145,7 @@ static void layer_decode(const std::vector<int>& prompt, int n_new, uint64_t see
         LLMI_CALL(llmi_memcpy(ids.p, &tok, 4, 0));
         launchInputEmbedding(&id_t, &dec_in, &E);
         step = pos + 1;  // llama.cpp: step = total length including this token
-        dec.forward<float>(in, lw, out, dp);
+        dec.forward(in, lw, out, dp);
         launchRMSNorm(&dec_out, &un, FN, 1e-5f, true);
         launchLinearGemm(&dec_out, LM, &probs, nullptr, false, true);
         launchTopKforBeamSearch(&probs, &next_t);
@@ -154,6 +154,52 @@ static void layer_decode(const std::vector<int>& prompt, int n_new, uint64_t see
     }
     std::printf("{\"layer_api_tokens\": [");
     for (size_t i = 0; i < gen.size(); ++i) std::printf("%s%d", i ? ", " : "", gen[i]);
+    std::printf("]}\n");
+
+    // ---- the same request with the prompt through LlamaContextDecoder in ONE batched
+    // pass (context_decoder.cpp:47-143, the reference's firstTokenGen path), then the
+    // self decoder from position n on (fresh fp32 caches)
+    const int n = (int)prompt.size();
+    Dev<float> kc2((size_t)L * kv * S * hd), vc2((size_t)L * kv * S * hd), xs((size_t)n * H), ys((size_t)n * H);
+    Dev<int> pids(prompt), hist(std::vector<int>{0}), qlen(std::vector<int>{n}), klen(std::vector<int>{n});
+    TensorWrapper<int> pid_t(GPU, INT32, {n}, pids.p), hist_t(GPU, INT32, {1}, hist.p), qlen_t(GPU, INT32, {1}, qlen.p),
+        klen_t(GPU, INT32, {1}, klen.p);
+    TensorWrapper<float> ctx_in(GPU, FP32, {n, H}, xs.p), ctx_out(GPU, FP32, {n, H}, ys.p);
+    TensorWrapper<float> kcache2(GPU, FP32, {L, 1, kv, S, hd}, kc2.p), vcache2(GPU, FP32, {L, 1, kv, S, hd}, vc2.p);
+    int layer0 = 0;
+    TensorWrapper<int> layer_t(CPU, INT32, {1}, &layer0);
+    launchInputEmbedding(&pid_t, &ctx_in, &E);
+    LlamaContextDecoder<half_t> ctx(heads, kv, hd, I, L, sp, 1e-5f, nullptr, nullptr, &g_alloc);
+    LLaMAAttentionDynParams cp;
+    cp.batch_size = 1;
+    cp.num_tokens = n;
+    cp.max_q_len = n;
+    cp.max_k_len = n;
+    cp.num_layers = L;
+    TensorMap cin{{"decoder_input", &ctx_in}, {"history_length", &hist_t}, {"input_length", &qlen_t},
+                  {"context_length", &klen_t}, {"layer_id", &layer_t}};
+    TensorMap cout{{"decoder_output", &ctx_out}, {"all_k_cache", &kcache2}, {"all_v_cache", &vcache2}};
+    ctx.forward(cin, lw, cout, cp);
+    TensorWrapper<float> last(GPU, FP32, {1, H}, ys.p + (size_t)(n - 1) * H);
+    launchRMSNorm(&last, &un, FN, 1e-5f, true);
+    launchLinearGemm(&last, LM, &probs, nullptr, false, true);
+    launchTopKforBeamSearch(&probs, &next_t);
+    LLMI_CALL(llmi_memcpy(&tok, next.p, 4, 1));
+    std::vector<int> gen2{tok};
+    TensorMap out2{{"decoder_output", &dec_out}, {"all_k_cache", &kcache2}, {"all_v_cache", &vcache2}};
+    for (int pos = n; pos < n + n_new - 1; ++pos) {
+        LLMI_CALL(llmi_memcpy(ids.p, &tok, 4, 0));
+        launchInputEmbedding(&id_t, &dec_in, &E);
+        step = pos + 1;
+        dec.forward(in, lw, out2, dp);
+        launchRMSNorm(&dec_out, &un, FN, 1e-5f, true);
+        launchLinearGemm(&dec_out, LM, &probs, nullptr, false, true);
+        launchTopKforBeamSearch(&probs, &next_t);
+        LLMI_CALL(llmi_memcpy(&tok, next.p, 4, 1));
+        gen2.push_back(tok);
+    }
+    std::printf("{\"context_layer_tokens\": [");
+    for (size_t i = 0; i < gen2.size(); ++i) std::printf("%s%d", i ? ", " : "", gen2[i]);
     std::printf("]}\n");
     for (auto* w : lw) delete w;
 }
