@@ -47,34 +47,96 @@ def algorithmic_bytes(weight_bytes: int, kv_per_pos: int, n_fwd: int) -> int:
     return n_fwd * weight_bytes + kv_per_pos * (ctx_sum + n_fwd)
 
 
-def cpu_baseline(sample_layers: int = 2, n_fwd: int = 48):
-    """Oracle (numpy, fp32) timed on this host: 7B width, `sample_layers` layers +
-    lm_head, n_fwd decode forwards at ctx 1..n_fwd; scaled to 32 layers."""
+def cpu_info():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_count": os.cpu_count(), "cpu_model": model}
+
+
+def cpu_baseline(sample_layers: int = 2, n_short: int = 12, n_long: int = 6, long_ctx: int = 1024):
+    """The numpy restatement of modeling_llama.py (oracle/llama_ref.py, fp32) on this
+    host, like-for-like with the GPU numbers (a bounded sample, scaled):
+      decode  (configs[1]): 7B width, `sample_layers` layers; forwards at ctx 1..n_short and,
+              with the cache pre-filled to long_ctx positions, at ctx long_ctx+1..+n_long. A
+              layer's time is linear in ctx (weights + attention over ctx), so the two samples
+              give its mean over the GPU run's ctx 1..2048; + lm_head; x 32 layers.
+      prefill (configs[2]): the same model, one 512-row batched prefill, x 32 layers.
+      int8_13b (configs[4]): 13B width, one W8A16 layer (dequantised to fp32), x 40 layers."""
     from threadpoolctl import threadpool_info
 
     from oracle import llama_ref as R
     from oracle import prng
-    cfg = R.LlamaConfig(layers=sample_layers, max_seq=n_fwd + 1)
+    threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    cfg = R.LlamaConfig(layers=sample_layers, max_seq=MAX_SEQ)
     o = R.LlamaOracle(cfg, seed=SEED)
     ids = prng.prompt_ids(SEED, PROMPT, cfg.vocab)
-    t0 = time.perf_counter()
-    logits = None
-    for i in range(n_fwd):
-        tok = int(ids[i]) if i < PROMPT else int(np.argmax(logits))
-        logits = o.forward_token(tok)
-    t_fwd = (time.perf_counter() - t0) / n_fwd
+
+    def fwd_time(n, pos0):
+        o.pos = pos0
+        logits, t = None, 0.0
+        for i in range(n):
+            tok = int(ids[i % PROMPT]) if logits is None or i < PROMPT else int(np.argmax(logits))
+            t0 = time.perf_counter()
+            logits = o.forward_token(tok)
+            t += time.perf_counter() - t0
+        return t / n
+
+    o.forward_token(int(ids[0]))  # warm the BLAS pools
+    t_short = fwd_time(n_short, 0)                      # ctx 1..n_short
+    rng = np.random.default_rng(SEED)
+    o.k_cache[:, :, :long_ctx] = rng.standard_normal(o.k_cache[:, :, :long_ctx].shape, dtype=np.float32)
+    o.v_cache[:, :, :long_ctx] = rng.standard_normal(o.v_cache[:, :, :long_ctx].shape, dtype=np.float32)
+    t_long = fwd_time(n_long, long_ctx)                 # ctx long_ctx+1..long_ctx+n_long
     x = o.last_hidden
     t0 = time.perf_counter()
-    for _ in range(n_fwd):
+    for _ in range(n_short):
         R.linear(R.rmsnorm(x, o.final_norm, cfg.rms_eps), o.lm_head)
-    t_head = (time.perf_counter() - t0) / n_fwd
-    t_layer = (t_fwd - t_head) / sample_layers
-    per_tok = t_head + 32 * t_layer
-    threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
-    return {"value": round(1.0 / per_tok, 4), "unit": "tokens/s", "cores": int(threads), "kind": "port",
-            "sample": f"numpy oracle (oracle/llama_ref.py, fp32), Llama-2-7B width, {sample_layers} layers + "
-                      f"lm_head, {n_fwd} greedy decode forwards at ctx 1..{n_fwd}; per-token time = lm_head + "
-                      f"32 x measured per-layer time ({t_layer * 1e3:.1f} ms/layer, {t_head * 1e3:.1f} ms head)"}
+    t_head = (time.perf_counter() - t0) / n_short
+    c_short, c_long = (n_short + 1) / 2, long_ctx + (n_long + 1) / 2
+    l_short, l_long = (t_short - t_head) / sample_layers, (t_long - t_head) / sample_layers
+    slope = (l_long - l_short) / (c_long - c_short)
+    l_mean = l_short + slope * ((MAX_SEQ + 1) / 2 - c_short)   # mean layer time over ctx 1..2048
+    per_tok = t_head + 32 * l_mean
+    out = {"value": round(1.0 / per_tok, 4), "unit": "tokens/s", "cores": int(threads), "kind": "port",
+           **cpu_info(), "ctx": f"1..{MAX_SEQ} (modelled from samples at ctx 1..{n_short} and "
+                                 f"{long_ctx + 1}..{long_ctx + n_long})",
+           "sample": f"numpy oracle (oracle/llama_ref.py, fp32 weights from the fp16 PRNG values), Llama-2-7B "
+                     f"width, {sample_layers} layers + lm_head; per-layer {l_short * 1e3:.1f} ms at ctx ~{c_short:.0f}, "
+                     f"{l_long * 1e3:.1f} ms at ctx ~{c_long:.0f}; lm_head {t_head * 1e3:.1f} ms; "
+                     f"per token = lm_head + 32 x mean layer time over ctx 1..{MAX_SEQ}"}
+    # configs[2]: one 512-row prefill on the same model
+    m = 512
+    o.pos = 0
+    t0 = time.perf_counter()
+    o.prefill(prng.prompt_ids(SEED + 1, m, cfg.vocab))
+    t_pf = time.perf_counter() - t0
+    pf_ms = (t_pf - t_head) / sample_layers * 32 * 1e3 + t_head * 1e3
+    out["prefill"] = {"ms": round(pf_ms, 1), "rows": m,
+                      "sample": f"oracle prefill of {m} rows, {sample_layers} layers ({t_pf * 1e3:.0f} ms), x 32 layers"}
+    del o
+    # configs[4]: one 13B-width int8 layer
+    c13 = R.LlamaConfig(hidden=5120, heads=40, kv_heads=40, inter=13824, layers=1, max_seq=64)
+    o13 = R.LlamaOracle(c13, seed=SEED, int8=True)
+    o13.forward_token(int(ids[0]))
+    t0 = time.perf_counter()
+    for i in range(n_long):
+        o13.forward_token(int(ids[i % PROMPT]))
+    t13 = (time.perf_counter() - t0) / n_long
+    x = o13.last_hidden
+    t0 = time.perf_counter()
+    for _ in range(n_long):
+        R.linear(R.rmsnorm(x, o13.final_norm, c13.rms_eps), o13.lm_head)
+    h13 = (time.perf_counter() - t0) / n_long
+    out["int8_13b"] = {"tokens_per_s": round(1.0 / (h13 + 40 * (t13 - h13)), 4),
+                       "sample": f"oracle, 13B width, 1 W8A16 layer (dequantised fp32) + lm_head, {n_long} forwards at "
+                                 f"ctx <= {n_long + 1}; per token = lm_head + 40 x layer time"}
+    return out
 
 
 def pmc_traffic(kernel: str):
@@ -122,8 +184,9 @@ def prefill_side(eng, prompt_len: int = 512, reps: int = 3):
     return out
 
 
-def int8_side(n_new: int = 256):
-    """Config 5 beside the headline: Llama-2-13B-shape int8 W8A16 single-stream decode."""
+def int8_side(n_new: int = MAX_SEQ - PROMPT + 1):
+    """Config 5 beside the headline: Llama-2-13B-shape int8 W8A16 single-stream decode,
+    over the same ctx 1..2048 as the headline (2048 forwards)."""
     import llmi
     from llmi.engine import Engine, preset, synth_prompt
     cfg = preset("llama2-13b", max_seq=PROMPT + n_new)
@@ -279,6 +342,9 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline()
+            if "prefill" in out and "exact" in out["prefill"]:
+                out["cpu_baseline"]["prefill"]["gpu_speedup_exact"] = round(
+                    out["cpu_baseline"]["prefill"]["ms"] / out["prefill"]["exact"]["ms"], 1)
         except Exception as e:  # reported, never fatal to the GPU number
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     print(json.dumps(out), flush=True)
