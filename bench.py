@@ -41,6 +41,11 @@ PROMPT = 8
 SEED = 0
 
 
+def progress(msg: str):
+    """Phase markers on stderr (a long silent run looks hung to a watchdog)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def algorithmic_bytes(weight_bytes: int, kv_per_pos: int, n_fwd: int) -> int:
     """Sum over forwards at ctx = 1..n_fwd of weights + KV read (ctx slots) + KV write (1 slot)."""
     ctx_sum = n_fwd * (n_fwd + 1) // 2
@@ -88,6 +93,7 @@ def cpu_baseline(sample_layers: int = 2, n_short: int = 12, n_long: int = 6, lon
         return t / n
 
     o.forward_token(int(ids[0]))  # warm the BLAS pools
+    progress("cpu baseline: decode samples")
     t_short = fwd_time(n_short, 0)                      # ctx 1..n_short
     rng = np.random.default_rng(SEED)
     o.k_cache[:, :, :long_ctx] = rng.standard_normal(o.k_cache[:, :, :long_ctx].shape, dtype=np.float32)
@@ -111,6 +117,7 @@ def cpu_baseline(sample_layers: int = 2, n_short: int = 12, n_long: int = 6, lon
                      f"{l_long * 1e3:.1f} ms at ctx ~{c_long:.0f}; lm_head {t_head * 1e3:.1f} ms; "
                      f"per token = lm_head + 32 x mean layer time over ctx 1..{MAX_SEQ}"}
     # configs[2]: one 512-row prefill on the same model
+    progress("cpu baseline: prefill sample")
     m = 512
     o.pos = 0
     t0 = time.perf_counter()
@@ -121,6 +128,7 @@ def cpu_baseline(sample_layers: int = 2, n_short: int = 12, n_long: int = 6, lon
                       "sample": f"oracle prefill of {m} rows, {sample_layers} layers ({t_pf * 1e3:.0f} ms), x 32 layers"}
     del o
     # configs[4]: one 13B-width int8 layer
+    progress("cpu baseline: int8 13B sample")
     c13 = R.LlamaConfig(hidden=5120, heads=40, kv_heads=40, inter=13824, layers=1, max_seq=64)
     o13 = R.LlamaOracle(c13, seed=SEED, int8=True)
     o13.forward_token(int(ids[0]))
@@ -261,11 +269,13 @@ def main():
         eng.set_prompt(prompt)
         eng.decode(n_fwd, use_graph=not args.eager)
 
+    progress(f"warmup x{args.warmup}")
     for _ in range(args.warmup):
         one_generation()
     eng.sync()
     barrier()
     eng.sync()
+    progress(f"timed x{args.steps}")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_generation()
@@ -286,14 +296,17 @@ def main():
         consistent = all(o == objs[0] for o in objs)
 
     wbytes, kvb = eng.bytes_per_token()
+    progress("kernel timings")
     # dominant kernel: gate_up GEMV, timed with HIP events on the engine stream
     gu_us, gu_bytes = eng.time_kernel("gate_up", iters=256)
     kern = {k: eng.time_kernel(k, iters=128) for k in ("qkv", "attn", "o", "down", "lm_head")}
     side = {}
     if world == 1 and not args.no_side:
+        progress("prefill side measurement")
         side["prefill"] = prefill_side(eng, prompt_len=512)
     eng.close()
     if world == 1 and not args.no_side:
+        progress("int8 13B side measurement")
         side["int8_13b"] = int8_side()
 
     if rank != 0:
@@ -341,6 +354,7 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         try:
+            progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline()
             if "prefill" in out and "exact" in out["prefill"]:
                 out["cpu_baseline"]["prefill"]["gpu_speedup_exact"] = round(

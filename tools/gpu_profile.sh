@@ -2,18 +2,22 @@
 # One GPU session: bench line, rocprofv3 kernel-trace stats of the same bench,
 # separate FETCH_SIZE / WRITE_SIZE PMC passes on the gate_up GEMV.
 # Usage (on the gpurun box): bash tools/gpu_profile.sh <tag>
+#   SKIP_PROFILE=1: tests + bench only;  SKIP_TESTS=1: profiles only
 set -o pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
+if [ -z "$SKIP_TESTS" ]; then
 echo "[$(date +%T)] pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed $?"; tail -30 $OUT/pytest_gpu_$TAG.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed $?"; tail -30 $OUT/pytest_gpu_$TAG.log; exit 1; }
 tail -2 $OUT/pytest_gpu_$TAG.log
 echo "[$(date +%T)] bench"
 timeout -k 10 600 python bench.py --steps 2 --warmup 1 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo "bench failed $?"; tail -20 $OUT/bench_$TAG.err; exit 1; }
 cat $OUT/bench_$TAG.json
+fi
+[ -n "$SKIP_PROFILE" ] && exit 0
 echo "[$(date +%T)] attention sweep"
 timeout -k 10 300 python3 tools/kernel_probe.py --layers 2 --iters 100 --loop --attn-sweep 8,64,65,128,256,512,1024,2047 > $OUT/probe_$TAG.json 2> $OUT/probe_$TAG.err || { echo "probe failed $?"; tail -20 $OUT/probe_$TAG.err; exit 1; }
 cat $OUT/probe_$TAG.json
@@ -24,10 +28,10 @@ find /tmp/prof_trace -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats_$TA
 python3 tools/trace_summary.py $(find /tmp/prof_trace -name '*kernel_trace.csv' | head -1) > $OUT/trace_summary_$TAG.json || echo "trace summary failed"
 echo "[$(date +%T)] pmc fetch"
 rm -rf /tmp/pmc_f /tmp/pmc_w
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'gemv_kernel' -d /tmp/pmc_f -o pmc --output-format csv -- python3 tools/kernel_probe.py --ctx 64 --kernels gate_up,qkv,lm_head > $OUT/pmc_fetch_$TAG.log 2>&1 || { echo "pmc fetch failed $?"; tail -20 $OUT/pmc_fetch_$TAG.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'gemv_kernel|attn_decode_kernel|attn_oproj_kernel' -d /tmp/pmc_f -o pmc --output-format csv -- python3 tools/kernel_probe.py --ctx 2048 --kernels gate_up,qkv,lm_head,attn,o,down > $OUT/pmc_fetch_$TAG.log 2>&1 || { echo "pmc fetch failed $?"; tail -20 $OUT/pmc_fetch_$TAG.log; exit 1; }
 find /tmp/pmc_f -name '*counter_collection.csv' -exec cp {} $OUT/pmc_fetch_$TAG.csv \;
 echo "[$(date +%T)] pmc write"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'gemv_kernel' -d /tmp/pmc_w -o pmc --output-format csv -- python3 tools/kernel_probe.py --ctx 64 --kernels gate_up,qkv,lm_head > $OUT/pmc_write_$TAG.log 2>&1 || { echo "pmc write failed $?"; tail -20 $OUT/pmc_write_$TAG.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'gemv_kernel|attn_decode_kernel|attn_oproj_kernel' -d /tmp/pmc_w -o pmc --output-format csv -- python3 tools/kernel_probe.py --ctx 2048 --kernels gate_up,qkv,lm_head,attn,o,down > $OUT/pmc_write_$TAG.log 2>&1 || { echo "pmc write failed $?"; tail -20 $OUT/pmc_write_$TAG.log; exit 1; }
 find /tmp/pmc_w -name '*counter_collection.csv' -exec cp {} $OUT/pmc_write_$TAG.csv \;
 echo "[$(date +%T)] prefill trace"
 rm -rf /tmp/prof_pf
