@@ -23,12 +23,19 @@ def main():
     ap.add_argument("--kernels", default="qkv,attn,o,gate_up,down,lm_head")
     ap.add_argument("--loop", action="store_true", help="also time a graph-replayed decode loop")
     ap.add_argument("--attn-sweep", default="", help="comma list of ctx values to time attention at")
+    ap.add_argument("--prefill", action="store_true",
+                    help="reach ctx with one batched prefill instead of ctx eager decode steps (few dispatches: "
+                         "for rocprofv3 --pmc passes)")
     a = ap.parse_args()
     cfg = preset("llama2-7b", layers=a.layers, max_seq=a.ctx)
     with Engine(cfg) as e:
         e.load_synthetic(0)
-        e.set_prompt(synth_prompt(0, 8, cfg.vocab))
-        e.decode(a.ctx, use_graph=False)  # leaves cur_pos = ctx - 1: attention runs at full ctx
+        if a.prefill:
+            e.set_prompt(synth_prompt(0, a.ctx, cfg.vocab))
+            e.prefill(a.ctx)  # leaves cur_pos = ctx - 1: attention runs at full ctx
+        else:
+            e.set_prompt(synth_prompt(0, 8, cfg.vocab))
+            e.decode(a.ctx, use_graph=False)  # leaves cur_pos = ctx - 1: attention runs at full ctx
         out = {"lib": os.environ.get("LLMI_LIB_PATH", "default")}
         if a.loop:
             import time

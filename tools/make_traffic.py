@@ -12,7 +12,9 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ALG = {"qkv": 100663296, "gate_up": 180355072, "down": 90177536, "lm_head": 262144000}
+# attention at ctx 2048 (kernel_probe --ctx 2048): 2 * 2048 * 32 * 128 * 2 B of K/V + the new slot
+ALG = {"qkv": 100663296, "gate_up": 180355072, "down": 90177536, "lm_head": 262144000, "attn": 33570816,
+       "o": 33554432}
 
 
 def role(name):
@@ -24,6 +26,10 @@ def role(name):
         return "lm_head"
     if "gemv_kernel<__half, 2, 4," in name:
         return "down"
+    if "attn_decode_kernel<__half>" in name:
+        return "attn"
+    if "attn_oproj_kernel<__half" in name:
+        return "o"
     return None
 
 
