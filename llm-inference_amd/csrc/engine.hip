@@ -98,9 +98,11 @@ struct Engine {
     int pf_rows = 0;
     float *pf_x = nullptr, *pf_qkv = nullptr, *pf_o = nullptr, *pf_act = nullptr;
     _Float16 *pf_ah = nullptr, *pf_al = nullptr;  // fp16 activation planes (gemm2 path)
-    float* pf_slab = nullptr;      // split-K partial slabs of the o_proj / down GEMMs [kPfSplit][R][H]
+    float* pf_slab = nullptr;      // split-K partial slabs of the o_proj / down GEMMs [kPfSlabs][R][H]
     int pf_pending = 0;            // slices in pf_slab not yet added into pf_x
-    static constexpr int kPfSplit = 2;
+    static constexpr int kPfSplit = 2;   // o_proj (gemm2) K slices
+    static constexpr int kPfDown = 8;    // down (gemm3) K slices
+    static constexpr int kPfSlabs = 8;
     int host_next_pos = 0, prompt_len = 0;
     unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
     uint64_t seed = 0;
@@ -686,10 +688,11 @@ struct Engine {
         const size_t R = pf_rows, A = 256;
         size_t off = 0;
         auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, A); return o; };
-        const size_t ox = take(R * c.hidden * 4), oq = take(R * (ql + 2 * kvrows) * 4), oo = take(R * ql * 4),
+        // qkv: two K slices of the gemm3 GEMM, summed by the rope kernel into slice 0
+        const size_t ox = take(R * c.hidden * 4), oq = take(2 * R * (ql + 2 * kvrows) * 4), oo = take(R * ql * 4),
                      oa = take(R * il * 4);
         const size_t wide = std::max<size_t>(std::max<size_t>(c.hidden, ql), il);
-        const size_t oh = take(R * wide * 2), ol = take(R * wide * 2), os = take(kPfSplit * R * c.hidden * 4);
+        const size_t oh = take(R * wide * 2), ol = take(R * wide * 2), os = take(kPfSlabs * R * c.hidden * 4);
         LLMI_HIP(hipMalloc(&pf, off));
         pf_slab = (float*)(pf + os);
         pf_ah = (_Float16*)(pf + oh);
@@ -716,11 +719,19 @@ struct Engine {
                                    pf_pending ? pf_slab : nullptr, pf_pending));
         pf_pending = 0;
         g.lda = H; g.w = L.qkv; g.n = ql + 2 * kvrows; g.k = H;
-        g.epi = EPI_STORE; g.y = pf_qkv; g.ldy = g.n;
-        LLMI_TRY(gemm2_launch(g, stream));
-        // rope + kv write + causal attention
+        g.ldy = g.n;
+        const bool qkv3 = gemm3_supported(g.n, H, EPI_SLAB, 2);
+        if (qkv3) {  // two K slices (96 tiles alone would leave most CUs idle)
+            g.epi = EPI_SLAB; g.ksplit = 2; g.slab = pf_qkv;
+            LLMI_TRY(gemm3_launch(g, stream));
+        } else {
+            g.epi = EPI_STORE; g.y = pf_qkv;
+            LLMI_TRY(gemm2_launch(g, stream));
+        }
+        // rope (+ the second qkv slice) + kv write + causal attention
         PrefillAttnArgs pa;
         pa.qkv = pf_qkv;
+        pa.qkv2 = qkv3 ? pf_qkv + (size_t)m * g.n : nullptr;
         pa.k_cache = (char*)kcache + (size_t)l * kv_layer_elems * eb;
         pa.v_cache = (char*)vcache + (size_t)l * kv_layer_elems * eb;
         pa.cache_dtype = c.kv_dtype; pa.max_seq = c.max_seq; pa.m = m; pa.p0 = p0;
@@ -743,13 +754,19 @@ struct Engine {
         g.lda = H; g.w = L.gu; g.n = 2 * il; g.k = H;
         g.epi = EPI_SILU_MUL; g.pair_off = il; g.y = nullptr; g.y_hi = pf_act_h(); g.y_lo = split == 2 ? pf_act_l() : nullptr;
         g.ldy = il;
-        LLMI_TRY(gemm2_launch(g, stream));
-        // down + residual
+        LLMI_TRY(gemm3_supported(g.n, H, EPI_SILU_MUL, 1) ? gemm3_launch(g, stream) : gemm2_launch(g, stream));
+        // down + residual: K slices into slabs (gemm3: 8 uneven slices, 256 workgroups)
         g.a[0] = pf_act_h(); g.a[1] = split == 2 ? pf_act_l() : nullptr;
-        const int sd = (il % (kPfSplit * 64)) == 0 ? kPfSplit : 1;
         g.lda = il; g.w = L.down; g.n = H; g.k = il;
-        g.epi = EPI_SLAB; g.ksplit = sd; g.pair_off = 0; g.y = pf_x; g.y_hi = g.y_lo = nullptr; g.ldy = H;
-        LLMI_TRY(gemm2_launch(g, stream));
+        g.epi = EPI_SLAB; g.pair_off = 0; g.y = pf_x; g.y_hi = g.y_lo = nullptr; g.ldy = H; g.slab = pf_slab;
+        int sd;
+        if (gemm3_supported(H, il, EPI_SLAB, kPfDown)) {
+            sd = kPfDown; g.ksplit = sd;
+            LLMI_TRY(gemm3_launch(g, stream));
+        } else {
+            sd = (il % (kPfSplit * 64)) == 0 ? kPfSplit : 1; g.ksplit = sd;
+            LLMI_TRY(gemm2_launch(g, stream));
+        }
         pf_pending = sd;  // added by the next layer's rows_split (or prefill_flush)
         return LLMI_OK;
     }

@@ -1,0 +1,340 @@
+// Prefill linear layers, second generation: 256 x 256 output tiles, 8 waves in two
+// ping-pong groups (the M = prompt-rows case of
+// launchLinearGemm, linear.cu:38-99, called from context_attention.cpp:99,166 and
+// ffn.cpp:72,89). Same operands, numerics and epilogues as gemm2.hip (Gemm2Args);
+// this file changes the schedule, which is what bounds gemm2 (27-32 % MFMA busy):
+//
+//  * bytes per FLOP. A 128 x 128 tile fetches 32 KB per 64-deep K step for 2 MFLOP;
+//    256 x 256 fetches 64 KB for 8 MFLOP (half the L2 -> CU traffic per FLOP).
+//  * the interleave. Each 64-deep K tile is four phases, one per 128 x 128 quadrant
+//    of the workgroup tile (all 8 waves, 64 x 32 each, 16 v_mfma_f32_16x16x32_f16).
+//    Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave issues
+//    its MFMAs while its partner issues the next phase's LDS reads and LDS-DMA
+//    (cdna_hip_programming.md, "The 256² 8-phase template").
+//  * the staging. The tile is four 16 KB half-images (A rows 0-127 / 128-255, W rows
+//    0-127 / 128-255) in two 64 KB buffers, filled by global_load_lds_dwordx4. One
+//    half-image is issued per phase, as soon as the previous occupant of its slot
+//    was read for the last time (+1 phase), four to five phases ahead of its first read; every phase
+//    waits a counted vmcnt (never 0 in the steady state) before the raw barrier.
+//
+// Hazard bookkeeping (phase n = 4 t + j of K tile t; group g's LDS reads of phase n
+// are issued before its first barrier of the phase and retired -- lgkmcnt -- right
+// after it, ahead of its MFMAs):
+//   MFMAs:   j0 (A0, B0), j1 (A0, B1), j2 (A1, B1), j3 (A1, B0)
+//   reads:   j0: A0 + B0 of tile t, j1: B1, j2: A1, j3: none (operands in registers)
+//   issues:  j0: B1 of tile t+1, j1: A1 of t+1, j2: A0 of t+2, j3: B0 of t+2
+//   each slot is re-filled two phases after its last read (by then both groups have
+//   retired those reads and passed a barrier), and every half-image is retired by the
+//   wait of the phase before its first read (the wait at phase n retires everything
+//   issued up to phase n - 4), published by the next barrier.
+// Measured alternatives that lost (tools/gemm_bench, same process A/B): the DMA issued
+// between the MFMAs instead of in the load slot (-4..-9 %), reads rebalanced 8/4/8/4
+// by pre-reading the next tile's B0 in j3 (-5..-8 %), the st_16x32 swizzle (2-way
+// conflicted fragment reads, -5..-10 %).
+// Exact mode (planes = 2): the lo plane is 2 K more K -- the K loop runs over
+// [hi | lo] against [W | W], so LDS and registers are those of the fp16 mode.
+// Roofline: MFMA (fp16 dense 2.5 PFLOP/s); FLOPs per launch 2 * M * N * K * planes.
+#include "kernels.h"
+
+namespace llmi {
+
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr int kT = 512;              // 8 waves: (wr, wc) = (w >> 2, w & 3)
+constexpr int kTile = 256;           // BM = BN
+constexpr int kK = 64;               // K per tile step (128-B LDS rows)
+constexpr int kHalf = 128 * 128;     // one half-image: 128 rows x 128 B
+constexpr int kBuf = 4 * kHalf;      // A0 A1 B0 B1
+constexpr int kLds = 2 * kBuf;       // 128 KB
+
+#ifndef LLMI_G3_EXP
+#define LLMI_G3_EXP 0  // timing experiments only: 1 no DMA in the loop, 2 no LDS reads, 3 no DMA waits
+#endif
+#ifndef LLMI_G3_LGKM_EARLY
+#define LLMI_G3_LGKM_EARLY 0
+#endif
+
+// LDS image swizzle (an involution): 16-B chunk c of 128-B row r is stored at chunk
+// c ^ ((r >> 1) & 7). A fragment ds_read_b128 (lane: row fr = lane & 15, chunk
+// 4 kk + (lane >> 4)) then puts the 16 lanes of each ds_read_b128 lane group on 16
+// distinct 16-B bank slots -- conflict-free (the st_16x32 XOR of gemm2 leaves it 2-way).
+#ifndef LLMI_G3_SWZ_OLD
+__device__ __forceinline__ int swz3(int b) { return b ^ (((b >> 8) & 7) << 4); }
+#else
+__device__ __forceinline__ int swz3(int b) { return b ^ (((b >> 9) & 1) << 5); }
+#endif
+
+__device__ __forceinline__ void glds(const void* g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+// vmcnt(c) for the counts the schedule produces (wave-uniform branch)
+__device__ __forceinline__ void wait_vm(int c) {
+    if (c >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (c >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (c >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (c >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void bar() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ float silu3(float v) { return v / (1.0f + expf(-v)); }
+
+template <int EPI>
+__global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w >> 2, wc = w & 3;  // wr is also the ping-pong group
+    const int fr = lane & 15, fq = lane >> 4;
+
+    // bijective XCD remap, then tile-major over split-K slices, row tiles fastest
+    // (the row tiles of one W stripe run together on one XCD: W read once into L2)
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int S = (EPI == EPI_SLAB) ? a.ksplit : 1;
+    const int tile = id / S, slice = id - tile * S;
+    const int m_tiles = (a.m + kTile - 1) / kTile;
+    const int rt = tile % m_tiles, ct = tile / m_tiles;
+    const int m0 = rt * kTile;
+    // slice s covers K tiles [s * KT_all / S, (s + 1) * KT_all / S) of each plane
+    const int KT_all = a.k / kK;
+    const int kt0 = slice * KT_all / S;
+    const int KTs = (slice + 1) * KT_all / S - kt0;  // K tiles per plane in this slice
+    const int KT = KTs * a.planes;                   // virtual K tiles ([hi | lo])
+
+    // per-thread DMA sources: instruction i of a half-image fills half-local bytes
+    // i * 8192 + 16 t, which hold logical byte swz3(.) of the image
+    size_t a_off[2][2], b_off[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int b = swz3(i * kT * 16 + t * 16);
+        const int row = b >> 7, cb = b & 127;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int m = min(m0 + h * 128 + row, a.m - 1);
+            a_off[h][i] = (size_t)m * a.lda * 2 + cb;
+            int n;
+            if (EPI == EPI_SILU_MUL)  // W half 0: gate columns g0 + row, half 1: their up rows
+                n = ct * 128 + row + (h ? a.pair_off : 0);
+            else
+                n = ct * kTile + h * 128 + row;
+            b_off[h][i] = (size_t)n * a.k * 2 + cb;
+        }
+    }
+    const char* abase[2] = {reinterpret_cast<const char*>(a.a[0]),
+                            reinterpret_cast<const char*>(a.planes == 2 ? a.a[1] : a.a[0])};
+    const char* wbase = reinterpret_cast<const char*>(a.w);
+    const unsigned lds0 = (unsigned)(uintptr_t)lds;
+
+    // issue the half-image `half` (0 A0, 1 A1, 2 B0, 3 B1) of virtual K tile v
+    auto issue = [&](int v, int half) {
+        if (v >= KT) return;
+#if LLMI_G3_EXP == 1
+        if (v >= 2) return;
+#endif
+        const int plane = v >= KTs ? 1 : 0;
+        const size_t k0b = (size_t)(kt0 + v - plane * KTs) * kK * 2;
+        const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (v & 1) * kBuf + half * kHalf + w * 1024);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const char* src = half < 2 ? abase[plane] + a_off[half][i] + k0b : wbase + b_off[half - 2][i] + k0b;
+            glds(src, dst + i * kT * 16);
+        }
+    };
+    // phase n issues: j0 B1 of t+1, j1 A1 of t+1, j2 A0 of t+2, j3 B0 of t+2 (t = n >> 2)
+    const int n_last = 4 * (KT - 2) + 1;  // last phase whose issue is in range
+    auto vm_count = [&](int n) {          // glds of this wave issued in phases n-3 .. n
+        const int c = min(n, n_last) - (n - 4);
+        return 2 * max(0, min(4, c));
+    };
+
+    f4v acc[2][2][4][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+    h8v af[4][2], b0[2][2], b1[2][2];
+    auto read_a = [&](const char* img) {
+#if LLMI_G3_EXP == 2
+        if (KT > 0) return;
+#endif
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                af[i][kk] = *reinterpret_cast<const h8v*>(img + swz3((wr * 64 + i * 16 + fr) * 128 + kk * 64 + fq * 16));
+    };
+    auto read_b = [&](const char* img, h8v (&bf)[2][2]) {
+#if LLMI_G3_EXP == 2
+        if (KT > 0) return;
+#endif
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                bf[j][kk] = *reinterpret_cast<const h8v*>(img + swz3((wc * 32 + j * 16 + fr) * 128 + kk * 64 + fq * 16));
+    };
+    auto mma = [&](f4v (&c)[4][2], h8v (&bf)[2][2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][kk], bf[j][kk], c[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto sync_reads = [&](int n) {  // DMA counted, then the barrier; LDS reads retire behind it
+#if LLMI_G3_LGKM_EARLY
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+#if LLMI_G3_EXP != 3 && LLMI_G3_EXP != 1
+        wait_vm(vm_count(n));
+#endif
+        bar();
+    };
+
+    // prologue: virtual phases -6 .. -1 = A0, B0, B1, A1 of tile 0, A0, B0 of tile 1
+    issue(0, 0); issue(0, 2); issue(0, 3); issue(0, 1);
+    issue(1, 0); issue(1, 2);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0 of tile 0
+    bar();
+    if (wr == 1) bar();  // ping-pong: group 1 one barrier behind
+
+    for (int kt = 0; kt < KT; ++kt) {
+        const char* buf = lds + (kt & 1) * kBuf;
+        const int n = 4 * kt;
+        // j0: quadrant (A0, B0)
+        read_a(buf);
+        read_b(buf + 2 * kHalf, b0);
+        issue(kt + 1, 3);
+        sync_reads(n);
+        mma(acc[0][0], b0);
+        bar();
+        // j1: quadrant (A0, B1)
+        read_b(buf + 3 * kHalf, b1);
+        issue(kt + 1, 1);
+        sync_reads(n + 1);
+        mma(acc[0][1], b1);
+        bar();
+        // j2: quadrant (A1, B1)
+        read_a(buf + kHalf);
+        issue(kt + 2, 0);
+        sync_reads(n + 2);
+        mma(acc[1][1], b1);
+        bar();
+        // j3: quadrant (A1, B0)
+        issue(kt + 2, 2);
+        sync_reads(n + 3);
+        mma(acc[1][0], b0);
+        bar();
+    }
+    if (wr == 0) bar();  // equal barrier counts
+
+    // epilogue: acc[qa][qb][i][j] register e is tile row qa*128 + wr*64 + 16 i + 4 fq + e,
+    // tile column qb*128 + wc*32 + 16 j + fr (SILU: qb 0 gate, qb 1 its up column)
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int m = m0 + qa * 128 + wr * 64 + 16 * i + 4 * fq + e;
+                if (m >= a.m) continue;
+                if (EPI == EPI_SILU_MUL) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int gc = ct * 128 + wc * 32 + 16 * j + fr;
+                        const float v = silu3(acc[qa][0][i][j][e]) * acc[qa][1][i][j][e];
+                        const size_t o = (size_t)m * a.ldy + gc;
+                        if (a.y_hi) {
+                            const _Float16 hi = (_Float16)v;
+                            a.y_hi[o] = hi;
+                            if (a.y_lo) a.y_lo[o] = (_Float16)(v - (float)hi);
+                        } else {
+                            a.y[o] = v;
+                        }
+                    }
+                } else {
+                    float* yrow = (EPI == EPI_SLAB ? a.slab + (size_t)slice * a.m * a.ldy : a.y) + (size_t)m * a.ldy;
+#pragma unroll
+                    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int n = ct * kTile + qb * 128 + wc * 32 + 16 * j + fr;
+                            if (EPI == EPI_ADD)
+                                yrow[n] += acc[qa][qb][i][j][e];
+                            else
+                                yrow[n] = acc[qa][qb][i][j][e];
+                        }
+                }
+            }
+}
+
+template <int EPI>
+int launch_g3(const Gemm2Args& a, int grid, hipStream_t s) {
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<EPI>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess;
+    }();
+    LLMI_REQUIRE(attr, "gemm3: cannot raise the dynamic LDS limit");
+    hipLaunchKernelGGL(gemm3_kernel<EPI>, dim3(grid), dim3(kT), kLds, s, a);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace
+
+bool gemm3_supported(int n, int k, int epi, int ksplit) {
+    const int ncols = (epi == EPI_SILU_MUL) ? n / 2 : n;
+    const int tile = (epi == EPI_SILU_MUL) ? 128 : kTile;
+    const int s = epi == EPI_SLAB ? ksplit : 1;
+    return n > 0 && k > 0 && s >= 1 && ncols % tile == 0 && k % kK == 0 && k / kK / s >= 2;  // slices may be uneven
+}
+
+int gemm3_launch(Gemm2Args a, hipStream_t s) {
+    LLMI_REQUIRE(a.a[0] && a.w && a.m > 0, "gemm3: null operand or empty M");
+    LLMI_REQUIRE(a.planes == 1 || (a.planes == 2 && a.a[1]), "gemm3: planes must be 1 or 2 (with a[1])");
+    if (a.epi != EPI_SLAB) a.ksplit = 1;
+    LLMI_REQUIRE(gemm3_supported(a.n, a.k, a.epi, a.ksplit),
+                 "gemm3: N a multiple of 256 (gate_up: 2 x 128), K a multiple of 64, >= 2 K tiles of 64 per slice");
+    LLMI_REQUIRE(a.w_kblock == 0, "gemm3: head-major W blocks are not supported");
+    LLMI_REQUIRE(a.epi == EPI_SILU_MUL ? (a.y || a.y_hi) : (a.epi == EPI_SLAB ? a.slab != nullptr : a.y != nullptr),
+                 "gemm3: null output");
+    LLMI_REQUIRE(a.lda % 8 == 0 && (reinterpret_cast<uintptr_t>(a.a[0]) & 15) == 0 &&
+                     (a.planes == 1 || (reinterpret_cast<uintptr_t>(a.a[1]) & 15) == 0),
+                 "gemm3: A planes must be 16-B aligned with lda % 8 == 0");
+    LLMI_REQUIRE((reinterpret_cast<uintptr_t>(a.w) & 15) == 0 && a.k % 8 == 0, "gemm3: W must be 16-B aligned");
+    LLMI_REQUIRE(a.epi != EPI_SILU_MUL || a.pair_off == a.n / 2, "gemm3: gate_up pair offset must be N / 2");
+    const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
+    a.n_tiles = ncols / ((a.epi == EPI_SILU_MUL) ? 128 : kTile);
+    const int grid = ((a.m + kTile - 1) / kTile) * a.n_tiles * a.ksplit;
+    switch (a.epi) {
+        case EPI_STORE: return launch_g3<EPI_STORE>(a, grid, s);
+        case EPI_ADD: return launch_g3<EPI_ADD>(a, grid, s);
+        case EPI_SILU_MUL: return launch_g3<EPI_SILU_MUL>(a, grid, s);
+        case EPI_SLAB: return launch_g3<EPI_SLAB>(a, grid, s);
+    }
+    LLMI_REQUIRE(false, "gemm3: epilogue must be store, add, silu_mul or slab");
+}
+
+}  // namespace llmi

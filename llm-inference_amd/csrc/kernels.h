@@ -99,6 +99,9 @@ struct Gemm2Args {
 };
 bool gemm2_supported(int n, int k, int epi);
 int gemm2_launch(Gemm2Args a, hipStream_t s);
+// the same GEMM on 256 x 256 tiles with a ping-pong 8-wave schedule (gemm3.hip)
+bool gemm3_supported(int n, int k, int epi, int ksplit);
+int gemm3_launch(Gemm2Args a, hipStream_t s);
 // rows of x (+= the ksplit slices of slab, in slice order, written back to x),
 // then optional RMSNorm, then fp16 planes hi[, lo] (hi null: the combine alone)
 int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,
@@ -109,6 +112,7 @@ int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_
 // [0, p0 + m] per row; see prefill.hip.
 struct PrefillAttnArgs {
     float* qkv = nullptr;          // [m, (heads + 2 kv) * D] fp32; q rotated in place
+    const float* qkv2 = nullptr;   // optional second K slice of qkv (same layout), added first
     void* k_cache = nullptr;       // layer base [kv_heads, max_seq, D]
     void* v_cache = nullptr;
     int cache_dtype = LLMI_F16;

@@ -32,19 +32,26 @@ __device__ __forceinline__ void store_c(float* p, float v) { *p = v; }
 __device__ __forceinline__ float load_c(const __half* p) { return __half2float(*p); }
 __device__ __forceinline__ float load_c(const float* p) { return *p; }
 
-// grid (M), block 256: row m of qkv [M, (heads + 2 kv) * D]
+// grid (M), block 256: row m of qkv [M, (heads + 2 kv) * D]; with qkv2 (the second
+// K slice of the qkv GEMM) each element is qkv + qkv2 first, and the summed, rotated q
+// is what stays in qkv
 template <typename KT>
-__global__ void rope_kv_prefill_kernel(float* qkv, int ld, int p0, int heads, int kv_heads, const float* rope_tab,
-                                       KT* k_cache, KT* v_cache, int max_seq) {
+__global__ void rope_kv_prefill_kernel(float* qkv, const float* qkv2, int ld, int p0, int heads, int kv_heads,
+                                       const float* rope_tab, KT* k_cache, KT* v_cache, int max_seq) {
     const int m = blockIdx.x, pos = p0 + m;
     float* row = qkv + (size_t)m * ld;
+    const float* row2 = qkv2 ? qkv2 + (size_t)m * ld : nullptr;
     const float2* cs = reinterpret_cast<const float2*>(rope_tab) + (size_t)pos * (D / 2);
     // q heads then k heads: pairs (i, i + D/2), same expression as attn_decode_kernel
     for (int e = threadIdx.x; e < (heads + kv_heads) * (D / 2); e += blockDim.x) {
         const int hh = e / (D / 2), i = e % (D / 2);
         const float c = cs[i].x, s = cs[i].y;
         float* p = row + (size_t)hh * D;
-        const float x0 = p[i], x1 = p[i + D / 2];
+        float x0 = p[i], x1 = p[i + D / 2];
+        if (row2) {
+            x0 += row2[(size_t)hh * D + i];
+            x1 += row2[(size_t)hh * D + i + D / 2];
+        }
         const float r0 = x0 * c - x1 * s, r1 = x1 * c + x0 * s;
         if (hh < heads) {
             p[i] = r0;
@@ -55,10 +62,11 @@ __global__ void rope_kv_prefill_kernel(float* qkv, int ld, int p0, int heads, in
             store_c(kc + i + D / 2, r1);
         }
     }
-    const float* v = row + (size_t)(heads + kv_heads) * D;
+    const size_t vo = (size_t)(heads + kv_heads) * D;
     for (int e = threadIdx.x; e < kv_heads * D; e += blockDim.x) {
         const int hh = e / D, d = e % D;
-        store_c(v_cache + ((size_t)hh * max_seq + pos) * D + d, v[e]);
+        const float v = row2 ? row[vo + e] + row2[vo + e] : row[vo + e];
+        store_c(v_cache + ((size_t)hh * max_seq + pos) * D + d, v);
     }
 }
 
@@ -429,7 +437,7 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
     const int ld = (a.heads + 2 * a.kv_heads) * D;
     const dim3 ga((a.m + QB - 1) / QB, a.heads);
     if (a.cache_dtype == LLMI_F16) {
-        hipLaunchKernelGGL(rope_kv_prefill_kernel<__half>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, ld, a.p0, a.heads,
+        hipLaunchKernelGGL(rope_kv_prefill_kernel<__half>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (__half*)a.k_cache, (__half*)a.v_cache, a.max_seq);
         if (a.mfma_planes) {
             const dim3 gm((a.m + QM - 1) / QM, a.heads);
@@ -447,7 +455,7 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
                                a.heads * D);
         }
     } else if (a.cache_dtype == LLMI_F32) {
-        hipLaunchKernelGGL(rope_kv_prefill_kernel<float>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, ld, a.p0, a.heads,
+        hipLaunchKernelGGL(rope_kv_prefill_kernel<float>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (float*)a.k_cache, (float*)a.v_cache, a.max_seq);
         hipLaunchKernelGGL(attn_prefill_kernel<float>, ga, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0, a.heads,
                            a.kv_heads, (const float*)a.k_cache, (const float*)a.v_cache, a.max_seq, a.out,

@@ -1,0 +1,156 @@
+// Prefill GEMM bench: gemm2 (128^2 tiles) vs gemm3 (256^2 ping-pong) on the
+// Llama-2-7B prefill shapes at M rows (default 512) and a 4096^3 square, random
+// fp16 operands, HIP-event timing; checks gemm3 against gemm2 (EPI_STORE).
+//   hipcc -std=c++17 -O2 -I include -I llm-inference_amd/csrc tools/gemm_bench/gemm_bench.cpp \
+//     -L llm-inference_amd/lib -lllmi -Wl,-rpath,$PWD/llm-inference_amd/lib -o tools/gemm_bench/gemm_bench
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+using namespace llmi;
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                          \
+        }                                                                          \
+    } while (0)
+
+__global__ void fill_kernel(_Float16* p, size_t n, unsigned seed, float scale) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u ^ seed;
+        x ^= x >> 15; x *= 2246822519u; x ^= x >> 13; x *= 3266489917u; x ^= x >> 16;
+        p[i] = (_Float16)(((x & 0xffffff) / 8388608.0f - 1.0f) * scale);
+    }
+}
+
+static void fill(_Float16* p, size_t n, unsigned seed, float scale) {
+    hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, 0, p, n, seed, scale);
+    CK(hipGetLastError());
+}
+
+struct Shape {
+    const char* name;
+    int n, k, epi, ksplit;
+};
+
+template <typename F>
+static float time_us(F f, int iters) {
+    for (int i = 0; i < 3; ++i) f();
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) f();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return 1e3f * ms / iters;
+}
+
+int main(int argc, char** argv) {
+    const int M = argc > 1 ? std::atoi(argv[1]) : 512;
+    const int iters = argc > 2 ? std::atoi(argv[2]) : 20;
+    const int check = argc > 3 ? std::atoi(argv[3]) : 1;
+    const std::string only = argc > 4 ? argv[4] : "";  // run only this shape (and planes = argv[5])
+    const int only_planes = argc > 5 ? std::atoi(argv[5]) : 0;
+    std::vector<Shape> shapes = {
+        {"qkv", 12288, 4096, EPI_STORE, 1},   {"qkv_s2", 12288, 4096, EPI_SLAB, 2},
+        {"o_s2", 4096, 4096, EPI_SLAB, 2},    {"o_s4", 4096, 4096, EPI_SLAB, 4},
+        {"o_s8", 4096, 4096, EPI_SLAB, 8},    {"gate_up", 22016, 4096, EPI_SILU_MUL, 1},
+        {"down_s2", 4096, 11008, EPI_SLAB, 2}, {"down_s4", 4096, 11008, EPI_SLAB, 4},
+        {"down_s8", 4096, 11008, EPI_SLAB, 8}, {"qkv_s3", 12288, 4096, EPI_SLAB, 3}, {"o_s16", 4096, 4096, EPI_SLAB, 16},
+        {"sq4096", 4096, 4096, EPI_STORE, 1},
+    };
+    size_t maxA = 0, maxW = 0, maxY = 0;
+    for (auto& s : shapes) {
+        const int m = std::string(s.name) == "sq4096" ? 4096 : M;
+        maxA = std::max(maxA, (size_t)m * s.k);
+        maxW = std::max(maxW, (size_t)s.n * s.k);
+        maxY = std::max(maxY, (size_t)m * s.n * (s.epi == EPI_SLAB ? s.ksplit : 1));
+    }
+    _Float16 *ah, *al, *w, *yh, *yl;
+    float *y2, *y3, *slab;
+    CK(hipMalloc(&ah, maxA * 2));
+    CK(hipMalloc(&al, maxA * 2));
+    CK(hipMalloc(&w, maxW * 2));
+    CK(hipMalloc(&y2, maxY * 4));
+    CK(hipMalloc(&y3, maxY * 4));
+    CK(hipMalloc(&slab, maxY * 4));
+    CK(hipMalloc(&yh, maxY * 2));
+    CK(hipMalloc(&yl, maxY * 2));
+    fill(ah, maxA, 1, 1.0f);
+    fill(al, maxA, 2, 1.0f / 2048);
+    fill(w, maxW, 3, 0.05f);
+    CK(hipDeviceSynchronize());
+
+    for (auto& s : shapes) {
+        if (!only.empty() && only != s.name) continue;
+        const int m = std::string(s.name) == "sq4096" ? 4096 : M;
+        for (int planes = 1; planes <= 2; ++planes) {
+            if (only_planes && planes != only_planes) continue;
+            Gemm2Args g;
+            g.a[0] = ah; g.a[1] = al; g.planes = planes; g.lda = s.k; g.w = w; g.m = m; g.n = s.n; g.k = s.k;
+            g.epi = s.epi; g.ksplit = s.ksplit; g.slab = slab; g.ldy = s.epi == EPI_SILU_MUL ? s.n / 2 : s.n;
+            g.pair_off = s.epi == EPI_SILU_MUL ? s.n / 2 : 0;
+            g.y_hi = s.epi == EPI_SILU_MUL ? yh : nullptr;
+            g.y_lo = s.epi == EPI_SILU_MUL && planes == 2 ? yl : nullptr;
+            g.y = y2;
+            const double flop = 2.0 * m * s.n * s.k * planes;
+            float us2 = -1.f;
+            if (gemm2_supported(s.n, s.k, s.epi) && (s.epi != EPI_SLAB || s.k % (s.ksplit * 64) == 0) && s.ksplit <= 8)
+                us2 = time_us([&] { gemm2_launch(g, 0); }, iters);
+            float us3 = -1.f;
+            if (gemm3_supported(s.n, s.k, s.epi, s.ksplit)) us3 = time_us([&] { gemm3_launch(g, 0); }, iters);
+            double err = -1;
+            if (check && us3 > 0) {
+                Gemm2Args c = g;
+                c.epi = s.epi == EPI_SLAB ? EPI_STORE : s.epi;
+                c.y_hi = c.y_lo = nullptr;
+                c.y = y2;
+                gemm2_launch(c, 0);
+                const size_t ny = (size_t)m * g.ldy;
+                std::vector<float> h2(ny), h3(ny, 0.f);
+                if (s.epi == EPI_SLAB) {  // the slices of the timed gemm3 launch, summed in order
+                    gemm3_launch(g, 0);
+                    CK(hipDeviceSynchronize());
+                    std::vector<float> sl(ny * s.ksplit);
+                    CK(hipMemcpy(sl.data(), slab, sl.size() * 4, hipMemcpyDeviceToHost));
+                    for (int q = 0; q < s.ksplit; ++q)
+                        for (size_t i = 0; i < ny; ++i) h3[i] += sl[q * ny + i];
+                } else {
+                    c.y = y3;
+                    gemm3_launch(c, 0);
+                    CK(hipDeviceSynchronize());
+                    CK(hipMemcpy(h3.data(), y3, ny * 4, hipMemcpyDeviceToHost));
+                }
+                CK(hipMemcpy(h2.data(), y2, ny * 4, hipMemcpyDeviceToHost));
+                double mx = 0, ref = 0;
+                for (size_t i = 0; i < ny; ++i) {
+                    mx = std::max(mx, (double)std::fabs(h2[i] - h3[i]));
+                    ref = std::max(ref, (double)std::fabs(h2[i]));
+                }
+                err = mx / (ref > 0 ? ref : 1);
+            }
+            std::printf(
+                "{\"shape\": \"%s\", \"m\": %d, \"n\": %d, \"k\": %d, \"planes\": %d, \"ksplit\": %d, \"gemm2_us\": %.2f, "
+                "\"gemm3_us\": %.2f, \"gemm2_tflops\": %.1f, \"gemm3_tflops\": %.1f, \"rel_err\": %.3g}\n",
+                s.name, m, s.n, s.k, planes, s.ksplit, us2, us3, us2 > 0 ? flop / us2 * 1e-6 : 0.0,
+                us3 > 0 ? flop / us3 * 1e-6 : 0.0, err);
+            std::fflush(stdout);
+        }
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
