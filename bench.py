@@ -221,6 +221,24 @@ def int8_side(n_new: int = MAX_SEQ - PROMPT + 1):
             "gate_up_GBps": round(gu_b / (gu_us * 1e-6) / 1e9, 1)}
 
 
+def tp_exchange_side(eng, layers, ms_per_token, wbytes):
+    """TP exchange budget: per token 2 * layers int64 all-reduces of the
+    hidden-size fixed-point residual (32 KB) plus one uint64 max over the lm_head
+    partials. Times the engine's own residual all-reduce on its RCCL communicator --
+    eagerly and replayed from one captured graph, as the decode step replays them (a
+    collective: every rank runs this) -- and sets calls x latency against the measured
+    ms per token and the per-rank weight stream."""
+    out = {"calls_per_token": 2 * layers + 1, "payload_bytes": 4096 * 8}
+    out["allreduce_us_eager"] = round(eng.time_kernel("allreduce", iters=200)[0], 2)
+    out["allreduce_us_graph"] = round(eng.time_kernel("allreduce_graph", iters=256)[0], 2)
+    lat = out["allreduce_us_graph"]
+    out["exchange_us_per_token_est"] = round(lat * out["calls_per_token"], 1)
+    out["ms_per_token"] = round(ms_per_token, 4)
+    out["weight_stream_us_per_token_at_6.2TBps"] = round(wbytes / 6.2e12 * 1e6, 1)
+    out["exchange_share_of_token"] = round(out["exchange_us_per_token_est"] / (ms_per_token * 1e3), 3)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +248,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-side", action="store_true", help="skip the prefill / int8-13B side measurements")
     ap.add_argument("--kv", choices=["f16", "f32"], default="f16")
+    ap.add_argument("--tp-exchange", action="store_true",
+                    help="world 1: give the engine a single-rank RCCL communicator (its all-reduces run in the "
+                         "decode graph) and time the TP exchange -- a rehearsal of the world > 1 side measurement")
     ap.add_argument("--eager", action="store_true",
                     help="launch kernels eagerly instead of replaying the hipGraph (profiling: rocprofv3 "
                          "kernel tracing of graph replays crashes on ROCm 7.2)")
@@ -252,6 +273,8 @@ def main():
         obj = [tp_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         tp_id = obj[0]
+    elif args.tp_exchange:  # world-1 rehearsal: a single-rank RCCL communicator in the engine
+        tp_id = tp_unique_id()
 
     cfg = preset("llama2-7b", max_seq=args.max_seq, tp_rank=rank, tp_world=world)
     cfg.kv_dtype = llmi.F16 if args.kv == "f16" else llmi.F32
@@ -301,6 +324,12 @@ def main():
     gu_us, gu_bytes = eng.time_kernel("gate_up", iters=256)
     kern = {k: eng.time_kernel(k, iters=128) for k in ("qkv", "attn", "o", "down", "lm_head")}
     side = {}
+    if tp_id is not None:
+        progress("tp exchange side measurement")
+        try:
+            side["tp_exchange"] = tp_exchange_side(eng, cfg.layers, elapsed * 1e3 / args.steps / n_fwd, wbytes)
+        except Exception as e:  # reported, never fatal to the GPU number
+            side["tp_exchange"] = {"error": repr(e)[:300]}
     if world == 1 and not args.no_side:
         progress("prefill side measurement")
         side["prefill"] = prefill_side(eng, prompt_len=512)
@@ -308,7 +337,6 @@ def main():
     if world == 1 and not args.no_side:
         progress("int8 13B side measurement")
         side["int8_13b"] = int8_side()
-
     if rank != 0:
         if dist is not None:
             dist.barrier()

@@ -73,6 +73,11 @@ int llmi_add_residual_rmsnorm(float* residual, float* decoder_out, const void* b
 int llmi_add_residual(const float* residual, float* decoder_out, int n_tokens, int hidden,
                       llmi_stream_t stream);
 
+/* Elementwise f16 <-> f32 (round to nearest even): no reference counterpart; the
+ * C++ mirror (include/llmi/kernels.h) stages TensorWrapper<half> activations of the
+ * reference's fp16 instantiation through the fp32 operators with it. */
+int llmi_convert(const void* src, int src_dtype, void* dst, int dst_dtype, size_t n, llmi_stream_t stream);
+
 /* launchAct (src/kernels/act_kernel.h:8-9): in [n, 2, inter] (gate then up),
  * out[n, i] = silu(gate) * up. */
 int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llmi_stream_t stream);
@@ -307,7 +312,10 @@ int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes
 llmi_stream_t llmi_engine_stream(llmi_engine* e);
 /* Time `iters` eager launches of one kernel (HIP events on the engine stream);
  * launch i runs layer i % layers, so its weights stream from HBM as in decode.
- * which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head.
+ * which: 0 qkv, 1 attn, 2 o, 3 gate_up, 4 down, 5 lm_head; 6 / 7 one TP residual
+ * all-reduce (RCCL int64, hidden elements; engines created with a tp_id) launched
+ * eagerly / replayed from one captured graph of `iters` calls -- a collective: every
+ * rank must make the same call.
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
 /* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built

@@ -1,9 +1,11 @@
 // The reference's operator API (src/kernels/*.h launchers), same names and
 // argument meaning, implemented over the llmi C ABI (include/llmi.h) -- so code
 // written against Mr-wang27/llm-inference's launchers compiles against this
-// header and runs the MI355X kernels. Activations are TensorWrapper<float>
-// (the reference's working instantiation, user_entry.cpp:21 / llama.h:207);
-// weights may be float, half_t or int8_t (+ per-row scales).
+// header and runs the MI355X kernels. Activations are TensorWrapper<float> (the
+// reference's working instantiation, user_entry.cpp:21 / llama.h:207) or
+// TensorWrapper<half_t> (its fp16 instantiation: staged through the fp32 operators by
+// llmi_convert, results rounded back to fp16); weights may be float, half_t or int8_t
+// (+ per-row scales).
 //
 // Differences, all deliberate and documented per launcher:
 //  * every launcher takes an optional trailing stream (hipStream_t as void*);
@@ -29,51 +31,95 @@ inline void* attn_workspace(int heads, int head_dim, int max_seq) {
     return ws;
 }
 inline int tokens_of(const Tensor* t) { return t->shape.size() >= 2 ? t->size() / t->shape.back() : 1; }
+
+// fp32 view of an activation tensor: TensorWrapper<float> as is; TensorWrapper<half_t>
+// converted into a per-slot device scratch buffer (load = copy the values in) and
+// written back rounded to fp16 by back()
+inline float* f32_scratch(int slot, size_t n) {
+    thread_local void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+    thread_local size_t cap[4] = {0, 0, 0, 0};
+    if (n * sizeof(float) > cap[slot]) {
+        if (buf[slot]) LLMI_CALL(llmi_device_free(buf[slot]));
+        LLMI_CALL(llmi_device_alloc(&buf[slot], n * sizeof(float)));
+        cap[slot] = n * sizeof(float);
+    }
+    return static_cast<float*>(buf[slot]);
+}
+template <typename AT> struct Act;
+template <> struct Act<float> {
+    float* p;
+    Act(TensorWrapper<float>* t, int, void*, bool) : p(t ? t->data : nullptr) {}
+    void back(void*) {}
+};
+template <> struct Act<half_t> {
+    TensorWrapper<half_t>* t;
+    float* p = nullptr;
+    Act(TensorWrapper<half_t>* t_, int slot, void* stream, bool load) : t(t_) {
+        if (!t) return;
+        p = f32_scratch(slot, t->size());
+        if (load) LLMI_CALL(llmi_convert(t->data, LLMI_F16, p, LLMI_F32, t->size(), stream));
+    }
+    void back(void* stream) {
+        if (t) LLMI_CALL(llmi_convert(p, LLMI_F32, t->data, LLMI_F16, t->size(), stream));
+    }
+};
 }  // namespace llmi_detail
 
 // input_embedding.h:6-9 -- out[t, :] = table[ids[t], :]
-template <typename T>
-void launchInputEmbedding(TensorWrapper<int>* input_ids, TensorWrapper<float>* output, EmbeddingWeight<T>* embed_table,
+template <typename AT, typename T>
+void launchInputEmbedding(TensorWrapper<int>* input_ids, TensorWrapper<AT>* output, EmbeddingWeight<T>* embed_table,
                           void* stream = nullptr) {
     LLM_CHECK_WITH_INFO(embed_table->shape.size() == 2, "embedding table must be [vocab, hidden]");
+    llmi_detail::Act<AT> out(output, 0, stream, false);
     LLMI_CALL(llmi_embedding(input_ids->data, input_ids->size(), embed_table->data,
                              llmiWeightDtype(getWeightType<T>()), embed_table->shape[0], embed_table->shape[1],
-                             output->data, stream));
+                             out.p, stream));
+    out.back(stream);
 }
 
 // rmsnorm_kernel.h:11-17 -- in place on decoder_out; decoder_residual <- pre-norm x
-template <typename T>
-void launchRMSNorm(TensorWrapper<float>* decoder_out, TensorWrapper<float>* decoder_residual,
+template <typename AT, typename T>
+void launchRMSNorm(TensorWrapper<AT>* decoder_out, TensorWrapper<AT>* decoder_residual,
                    LayerNormWeight<T>& attn_norm_weight, float eps, bool is_last = false, void* stream = nullptr) {
     (void)is_last;
     const int hidden = decoder_out->shape.back();
-    LLMI_CALL(llmi_rmsnorm(decoder_out->data, decoder_out->data, decoder_residual ? decoder_residual->data : nullptr,
-                           attn_norm_weight.gamma, llmiWeightDtype(getWeightType<T>()),
+    llmi_detail::Act<AT> out(decoder_out, 0, stream, true), res(decoder_residual, 1, stream, false);
+    LLMI_CALL(llmi_rmsnorm(out.p, out.p, res.p, attn_norm_weight.gamma, llmiWeightDtype(getWeightType<T>()),
                            llmi_detail::tokens_of(decoder_out), hidden, eps, stream));
+    out.back(stream);
+    res.back(stream);
 }
 
 // fused_addresidual_norm.h:9-15 -- residual += decoder_out (+bias); decoder_out = rmsnorm(residual) * scale
-template <typename T>
-void launchFusedAddBiasResidualRMSNorm(TensorWrapper<float>* residual, TensorWrapper<float>* decoder_out,
+template <typename AT, typename T>
+void launchFusedAddBiasResidualRMSNorm(TensorWrapper<AT>* residual, TensorWrapper<AT>* decoder_out,
                                        BaseWeight<T>& norm, T* scale, float eps, void* stream = nullptr) {
     const int hidden = decoder_out->shape.back();
     const int dt = llmiWeightDtype(getWeightType<T>());
-    LLMI_CALL(llmi_add_residual_rmsnorm(residual->data, decoder_out->data, norm.bias, dt, scale, dt,
-                                        llmi_detail::tokens_of(decoder_out), hidden, eps, stream));
+    llmi_detail::Act<AT> res(residual, 0, stream, true), out(decoder_out, 1, stream, true);
+    LLMI_CALL(llmi_add_residual_rmsnorm(res.p, out.p, norm.bias, dt, scale, dt, llmi_detail::tokens_of(decoder_out),
+                                        hidden, eps, stream));
+    res.back(stream);
+    out.back(stream);
 }
 
 // add_residual.h:8-13 -- decoder_out += residual
-inline void launchAddResidual(TensorWrapper<float>* residual, TensorWrapper<float>* decoder_out, bool is_print = false,
-                              void* stream = nullptr) {
+template <typename AT>
+void launchAddResidual(TensorWrapper<AT>* residual, TensorWrapper<AT>* decoder_out, bool is_print = false,
+                       void* stream = nullptr) {
     (void)is_print;
-    LLMI_CALL(llmi_add_residual(residual->data, decoder_out->data, llmi_detail::tokens_of(decoder_out),
-                                decoder_out->shape.back(), stream));
+    llmi_detail::Act<AT> res(residual, 0, stream, true), out(decoder_out, 1, stream, true);
+    LLMI_CALL(llmi_add_residual(res.p, out.p, llmi_detail::tokens_of(decoder_out), decoder_out->shape.back(), stream));
+    out.back(stream);
 }
 
 // act_kernel.h:8-9 -- input [n, 2, inter] (gate, up) -> out [n, inter] = silu(gate) * up
-inline void launchAct(TensorWrapper<float>* input, TensorWrapper<float>* out, void* stream = nullptr) {
+template <typename AT>
+void launchAct(TensorWrapper<AT>* input, TensorWrapper<AT>* out, void* stream = nullptr) {
     LLM_CHECK_WITH_INFO(input->shape.size() == 3 && input->shape[1] == 2, "launchAct input must be [n, 2, inter]");
-    LLMI_CALL(llmi_silu_mul(input->data, out->data, input->shape[0], input->shape[2], stream));
+    llmi_detail::Act<AT> in(input, 0, stream, true), o(out, 1, stream, false);
+    LLMI_CALL(llmi_silu_mul(in.p, o.p, input->shape[0], input->shape[2], stream));
+    o.back(stream);
 }
 
 // cublasWrapper stand-in: the reference's launchLinearGemm takes one (linear.h:16-22);
@@ -85,8 +131,8 @@ struct cublasWrapper {
 // linear.h:16-22 -- output[m, n] = input[m, k] * weight[n, k]^T. The reference's
 // layers always pass trans_b = true for weights (masked_self_attention.cpp:62);
 // trans_a is not supported (it was unused on the decode path).
-template <typename T>
-void launchLinearGemm(TensorWrapper<float>* input, BaseWeight<T>& weight, TensorWrapper<float>* output,
+template <typename AT, typename T>
+void launchLinearGemm(TensorWrapper<AT>* input, BaseWeight<T>& weight, TensorWrapper<AT>* output,
                       cublasWrapper* cublas_wrapper = nullptr, bool trans_a = false, bool trans_b = true) {
     LLM_CHECK_WITH_INFO(!trans_a, "launchLinearGemm: trans_a is not supported");
     LLM_CHECK_WITH_INFO(trans_b, "launchLinearGemm: weights are [out, in] (trans_b = true)");
@@ -94,29 +140,34 @@ void launchLinearGemm(TensorWrapper<float>* input, BaseWeight<T>& weight, Tensor
     const int k = weight.shape[1], n = weight.shape[0];
     const int m = input->size() / k;
     LLM_CHECK_WITH_INFO(m * k == input->size(), "launchLinearGemm: input size is not a multiple of in_features");
-    LLMI_CALL(llmi_linear(input->data, weight.data, llmiWeightDtype(getWeightType<T>()), weight.scale, output->data,
-                          m, n, k, cublas_wrapper ? cublas_wrapper->stream : nullptr));
+    void* stream = cublas_wrapper ? cublas_wrapper->stream : nullptr;
+    llmi_detail::Act<AT> in(input, 0, stream, true), out(output, 1, stream, false);
+    LLMI_CALL(llmi_linear(in.p, weight.data, llmiWeightDtype(getWeightType<T>()), weight.scale, out.p, m, n, k, stream));
+    out.back(stream);
 }
 
 // qkv_bias_and_RoPE.h:40-42 -- one decode token, in place on q and k of the fused
 // qkv row [1, qkv_head_num, head_size] at position step - 1 (step: host tensor).
 // The reference assumed MHA (head_num = qkv_head_num / 3, :416); kv_head_num may be given.
-inline void launchRoPE(TensorWrapper<float>* qkv_buf, TensorWrapper<int>* step, LLaMAAttentionStaticParams& params,
-                       int kv_head_num = -1, void* stream = nullptr) {
+template <typename AT>
+void launchRoPE(TensorWrapper<AT>* qkv_buf, TensorWrapper<int>* step, LLaMAAttentionStaticParams& params,
+                int kv_head_num = -1, void* stream = nullptr) {
     const int qkv_heads = qkv_buf->shape[qkv_buf->shape.size() - 2];
     const int head_size = qkv_buf->shape.back();
     const int kv = kv_head_num > 0 ? kv_head_num : qkv_heads / 3;
-    LLMI_CALL(llmi_rope_decode(qkv_buf->data, step->getVal() - 1, qkv_heads - 2 * kv, kv, head_size,
-                               params.rotary_embedding_base, stream));
+    llmi_detail::Act<AT> q(qkv_buf, 0, stream, true);
+    LLMI_CALL(llmi_rope_decode(q.p, step->getVal() - 1, qkv_heads - 2 * kv, kv, head_size, params.rotary_embedding_base,
+                               stream));
+    q.back(stream);
 }
 
 // fused_decoder_self_attention.h:10-19 -- write k, v of the (already rotated) fused qkv
 // into cache slot step - 1 of layer layer_id, then masked MHA over positions
 // 0..step-1. caches [layers, batch(=1), kv_heads, max_seq, head] f32 or f16 bits.
-template <typename T, typename CT>
-void launchDecoderMaskedMHA(TensorWrapper<float>* qkv_buf, BaseWeight<T>& qkv, TensorWrapper<int>* layer_id,
+template <typename AT, typename T, typename CT>
+void launchDecoderMaskedMHA(TensorWrapper<AT>* qkv_buf, BaseWeight<T>& qkv, TensorWrapper<int>* layer_id,
                             TensorWrapper<CT>* k_cache, TensorWrapper<CT>* v_cache, TensorWrapper<bool>* finished,
-                            TensorWrapper<int>* step, TensorWrapper<float>* mha_output,
+                            TensorWrapper<int>* step, TensorWrapper<AT>* mha_output,
                             LLaMAAttentionStaticParams& static_params, void* stream = nullptr) {
     (void)qkv;
     (void)finished;
@@ -127,17 +178,19 @@ void launchDecoderMaskedMHA(TensorWrapper<float>* qkv_buf, BaseWeight<T>& qkv, T
     const int heads = qkv_heads - 2 * kv;
     const int cdt = llmiDtype(getTensorType<CT>());
     void* ws = llmi_detail::attn_workspace(heads, head, max_seq);
-    LLMI_CALL(llmi_attn_decode(qkv_buf->data, k_cache->data, v_cache->data, cdt, layer_id->getVal(), max_seq,
-                               step->getVal() - 1, heads, kv, head, /*rope=*/0, static_params.rotary_embedding_base,
-                               mha_output->data, ws, stream));
+    llmi_detail::Act<AT> q(qkv_buf, 0, stream, true), out(mha_output, 1, stream, false);
+    LLMI_CALL(llmi_attn_decode(q.p, k_cache->data, v_cache->data, cdt, layer_id->getVal(), max_seq, step->getVal() - 1,
+                               heads, kv, head, /*rope=*/0, static_params.rotary_embedding_base, out.p, ws, stream));
+    out.back(stream);
 }
 
 // topK.h:51-56 + sampling.h:12-18 as Llama<T> wires them: beam width 1 and
 // K = 1 (llama.cpp:59, sampling.cu:99), i.e. greedy argmax of probs [1, vocab];
 // final_topk_id receives the token id (device int).
-inline void launchTopKforBeamSearch(TensorWrapper<float>* probs, TensorWrapper<int>* final_topk_id,
-                                    void* stream = nullptr) {
-    LLMI_CALL(llmi_argmax(probs->data, probs->shape.back(), final_topk_id->data, stream));
+template <typename AT>
+void launchTopKforBeamSearch(TensorWrapper<AT>* probs, TensorWrapper<int>* final_topk_id, void* stream = nullptr) {
+    llmi_detail::Act<AT> p(probs, 0, stream, true);
+    LLMI_CALL(llmi_argmax(p.p, probs->shape.back(), final_topk_id->data, stream));
 }
 
 // topK.h:51-56 -- the reference's full signature. topk_ids / topK_values are the

@@ -43,6 +43,10 @@ int llmi_add_residual(const float* residual, float* decoder_out, int n_tokens, i
     return add_resid_launch(residual, decoder_out, n_tokens, hidden, STREAM(stream));
 }
 
+int llmi_convert(const void* src, int src_dtype, void* dst, int dst_dtype, size_t n, llmi_stream_t stream) {
+    return convert_launch(src, src_dtype, dst, dst_dtype, n, STREAM(stream));
+}
+
 int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llmi_stream_t stream) {
     return silu_mul_launch(gate_up, out, n_tokens, inter, STREAM(stream));
 }

@@ -1191,9 +1191,16 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             case 3: return llmi::gemv_launch(g.gu_args(l), g.stream);
             case 4: return llmi::gemv_launch(g.down_args(l), g.stream);
             case 5: return llmi::gemv_launch(g.lm_args(), g.stream);
+            case 6:
+            case 7: {  // the per-token TP exchange: one residual all-reduce (int64, hidden)
+                ncclResult_t r = ncclAllReduce(g.xacc, g.xacc, H, ncclInt64, ncclSum, g.comm, g.stream);
+                LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
+                return LLMI_OK;
+            }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..5");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..7");
     };
+    LLMI_REQUIRE(which < 6 || g.comm != nullptr, "time_kernel: the all-reduce needs an RCCL communicator (tp_id)");
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
         case 0: b = (uint64_t)(g.ql + 2 * g.kvrows) * H * ws + (g.ql + 2 * g.kvrows) * sc; break;
@@ -1208,6 +1215,8 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
         case 3: b = (uint64_t)2 * g.il * H * ws + 2 * g.il * sc; break;
         case 4: b = (uint64_t)H * g.il * ws + H * sc; break;
         case 5: b = (uint64_t)g.vl * H * g.esz; break;
+        case 6:
+        case 7: b = (uint64_t)H * 8; break;
     }
     // timing launches modify the residual stream (o/down epilogues add into x),
     // so save and restore the small activation state around them
@@ -1217,17 +1226,32 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     for (int i = 0; i < 3; ++i)
         LLMI_HIP(hipMemcpyAsync(save_fx.data() + i * H * 8, fx[i], H * 8, hipMemcpyDeviceToHost, g.stream));
     LLMI_TRY(launch());  // warm
+    hipGraph_t cg = nullptr;
+    hipGraphExec_t ce = nullptr;
+    if (which == 7) {  // the all-reduces captured into one graph, as the decode step replays them
+        LLMI_HIP(hipStreamBeginCapture(g.stream, hipStreamCaptureModeThreadLocal));
+        for (int i = 0; i < iters; ++i) LLMI_TRY(launch());
+        LLMI_HIP(hipStreamEndCapture(g.stream, &cg));
+        LLMI_HIP(hipGraphInstantiate(&ce, cg, nullptr, nullptr, 0));
+        LLMI_HIP(hipGraphLaunch(ce, g.stream));  // warm
+    }
     hipEvent_t t0, t1;
     LLMI_HIP(hipEventCreate(&t0));
     LLMI_HIP(hipEventCreate(&t1));
     LLMI_HIP(hipEventRecord(t0, g.stream));
-    for (int i = 0; i < iters; ++i) LLMI_TRY(launch());
+    if (ce) {
+        LLMI_HIP(hipGraphLaunch(ce, g.stream));
+    } else {
+        for (int i = 0; i < iters; ++i) LLMI_TRY(launch());
+    }
     LLMI_HIP(hipEventRecord(t1, g.stream));
     LLMI_HIP(hipEventSynchronize(t1));
     float ms = 0.f;
     LLMI_HIP(hipEventElapsedTime(&ms, t0, t1));
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
+    if (ce) (void)hipGraphExecDestroy(ce);
+    if (cg) (void)hipGraphDestroy(cg);
     LLMI_HIP(hipMemcpy(g.x, save.data(), H * 4, hipMemcpyHostToDevice));
     for (int i = 0; i < 3; ++i) LLMI_HIP(hipMemcpy(fx[i], save_fx.data() + i * H * 8, H * 8, hipMemcpyHostToDevice));
     *avg_us = ms * 1000.f / iters;

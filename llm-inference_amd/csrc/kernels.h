@@ -261,6 +261,7 @@ int repeat_kv_launch(const void* k_cache, const void* v_cache, int dtype, int la
 
 // ---------------------------------------------------------- synthetic
 // in-place reduction over W rank buffers (device array of pointers); op 0 i64 sum, 1 f32 sum, 2 u64 max
+int convert_launch(const void* src, int src_dtype, void* dst, int dst_dtype, size_t n, hipStream_t s);
 int group_reduce_launch(void* const* dev_bufs, int W, int n, int op, hipStream_t s);
 int synth_fill_launch(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
                       int cols, int row0, int col0, int ld, hipStream_t s);

@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstring>
 
+#include <algorithm>
+
 #include "kernels.h"
 #include "prng.h"
 
@@ -285,6 +287,29 @@ int add_resid_rmsnorm_launch(float* resid, float* out, const void* bias, int b_d
     LLMI_REQUIRE(resid && out && gamma && n > 0 && hidden > 0, "add_residual_rmsnorm: bad arguments");
     hipLaunchKernelGGL(add_resid_rmsnorm_kernel, dim3(n), dim3(kT), 0, s, resid, out, bias, b_dtype, gamma,
                        g_dtype, hidden, eps);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+// f16 <-> f32 elementwise (RNE on the way down): the C++ mirror's fp16-activation
+// launchers stage TensorWrapper<half> activations through the fp32 operators
+__global__ void convert_kernel(const void* src, int sdt, void* dst, int ddt, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float v = sdt == LLMI_F16 ? __half2float(static_cast<const __half*>(src)[i]) : static_cast<const float*>(src)[i];
+        if (ddt == LLMI_F16)
+            static_cast<__half*>(dst)[i] = __float2half_rn(v);
+        else
+            static_cast<float*>(dst)[i] = v;
+    }
+}
+
+int convert_launch(const void* src, int src_dtype, void* dst, int dst_dtype, size_t n, hipStream_t s) {
+    LLMI_REQUIRE((src_dtype == LLMI_F16 || src_dtype == LLMI_F32) && (dst_dtype == LLMI_F16 || dst_dtype == LLMI_F32),
+                 "convert: dtypes must be f16 or f32");
+    LLMI_REQUIRE(n == 0 || (src && dst), "convert: null buffer");
+    if (n == 0) return LLMI_OK;
+    const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(convert_kernel, dim3(grid), dim3(256), 0, s, src, src_dtype, dst, dst_dtype, n);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }

@@ -42,6 +42,7 @@ _SIGS = {
     "llmi_add_residual_rmsnorm": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _F, _P]),
     "llmi_add_residual": (_I, [_P, _P, _I, _I, _P]),
     "llmi_silu_mul": (_I, [_P, _P, _I, _I, _P]),
+    "llmi_convert": (_I, [_P, _I, _P, _I, _SZ, _P]),
     "llmi_linear": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _P]),
     "llmi_rope_decode": (_I, [_P, _I, _I, _I, _I, _F, _P]),
     "llmi_attn_workspace_bytes": (_SZ, [_I, _I, _I]),

@@ -123,7 +123,10 @@ class Engine:
     def stream(self) -> int:
         return _lib.lib().llmi_engine_stream(self._h) or 0
 
-    KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5}
+    # allreduce / allreduce_graph: one residual all-reduce of the TP exchange (needs a tp_id),
+    # launched eagerly / replayed from a captured graph of `iters` calls
+    KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5, "allreduce": 6,
+               "allreduce_graph": 7}
 
     def time_kernel(self, which: str, iters: int = 50):
         us, b = C.c_float(), C.c_uint64()
