@@ -99,6 +99,8 @@ struct Engine {
     float *pf_x = nullptr, *pf_qkv = nullptr, *pf_o = nullptr, *pf_act = nullptr;
     _Float16 *pf_ah = nullptr, *pf_al = nullptr;  // fp16 activation planes (gemm2 path)
     float* pf_slab = nullptr;      // split-K partial slabs of the o_proj / down GEMMs [kPfSlabs][R][H]
+    float* pf_split = nullptr;     // split-key prefill attention partials
+    size_t pf_split_floats = 0;
     int pf_pending = 0;            // slices in pf_slab not yet added into pf_x
     static constexpr int kPfSplit = 2;   // o_proj (gemm2) K slices
     static constexpr int kPfDown = 8;    // down (gemm3) K slices
@@ -693,8 +695,12 @@ struct Engine {
                      oa = take(R * il * 4);
         const size_t wide = std::max<size_t>(std::max<size_t>(c.hidden, ql), il);
         const size_t oh = take(R * wide * 2), ol = take(R * wide * 2), os = take(kPfSlabs * R * c.hidden * 4);
+        // split-key attention partials: [heads][R / 64][8 chunks][64 x 128 + 128] fp32
+        pf_split_floats = (size_t)hl * ((R + 63) / 64) * 8 * (64 * 128 + 128);
+        const size_t osp = take(pf_split_floats * 4);
         LLMI_HIP(hipMalloc(&pf, off));
         pf_slab = (float*)(pf + os);
+        pf_split = (float*)(pf + osp);
         pf_ah = (_Float16*)(pf + oh);
         pf_al = (_Float16*)(pf + ol);
         pf_x = (float*)(pf + ox);
@@ -738,6 +744,7 @@ struct Engine {
         pa.heads = hl; pa.kv_heads = kvl; pa.head_dim = c.head_dim; pa.rope_tab = rope_tab; pa.out = pf_o;
         if (c.kv_dtype == LLMI_F16) {  // MFMA attention writes the o_proj input planes itself
             pa.mfma_planes = split; pa.out_hi = pf_ah; pa.out_lo = lo;
+            pa.split_ws = pf_split; pa.split_ws_floats = pf_split_floats;
         }
         LLMI_TRY(prefill_attn_launch(pa, stream));
         // o_proj + residual

@@ -126,6 +126,9 @@ struct PrefillAttnArgs {
     int mfma_planes = 0;
     _Float16* out_hi = nullptr;
     _Float16* out_lo = nullptr;
+    // MFMA form: scratch for the split-key partials (null: one workgroup per query block)
+    float* split_ws = nullptr;
+    size_t split_ws_floats = 0;
 };
 int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s);
 // after a prefill of prompt rows [p0, p0 + n): record them as tokens and

@@ -16,6 +16,8 @@
 // Roofline: the attention is ~2.1 GFLOP per 7B layer at M = 512 (4 * heads *
 // d * M^2 / 2), bound by LDS operand traffic in this fp32 form; the GEMMs
 // around it dominate prefill (gemm.hip).
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace llmi {
@@ -210,11 +212,24 @@ constexpr int QM = 64;  // query rows per workgroup
 __device__ __forceinline__ int vswz(int d) { return (d ^ (d >> 3)) & 7; }  // Vt row d's 16-B chunk XOR
 constexpr int KB = 64;  // keys per block
 
+// Split keys: the causal range of query block qb (key blocks [0, nkb(qb))) is cut into
+// chunks of cb key blocks, one workgroup each, so the longest query blocks no longer set
+// the kernel's critical path (8 dependent key blocks at M = 512). A query block with one
+// chunk writes its output directly; otherwise every chunk writes its unnormalised
+// (O, m, l) to ws[head][qb][chunk] and attn_prefill_merge_kernel combines them in
+// chunk order. blockIdx.x enumerates (qb, chunk), longest query blocks first.
+__host__ __device__ inline int pf_nkb(int qb, int p0, int m_rows) {
+    const int kend = p0 + (qb * QM + QM < m_rows ? qb * QM + QM : m_rows);
+    return (kend + KB - 1) / KB;
+}
+constexpr int kPartFloats = QM * D + 2 * QM;  // one chunk's O rows, then m, then l
+
 template <int P>
 __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float* qkv, int ld, int m_rows, int p0,
                                                                      int heads, int kv_heads, const __half* k_cache,
                                                                      const __half* v_cache, int max_seq, float* out,
-                                                                     _Float16* out_hi, _Float16* out_lo, int ldo) {
+                                                                     _Float16* out_hi, _Float16* out_lo, int ldo,
+                                                                     int cb, float* ws, int maxc) {
     __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 + D * KB * 2 + 4 * P * 16 * KB * 2];
     char* Ks = smem;                 // [key][256 B], chunk ^= key & 15
     char* Vt = smem + KB * D * 2;    // [dim][128 B], chunk ^= vswz(dim)
@@ -222,7 +237,16 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
     const int fr = lane & 15, fq = lane >> 4;
     char* Pw = Vt + D * KB * 2 + w * P * 16 * KB * 2;  // this wave's [P][16][128 B], chunk ^= row & 7
 
-    const int qb = gridDim.x - 1 - blockIdx.x;  // longest (latest) query blocks first
+    const int nqb = (m_rows + QM - 1) / QM;
+    int qb = nqb - 1, chunk = 0, nch = 1;
+    for (int idx = blockIdx.x; qb >= 0; --qb) {  // longest (latest) query blocks first
+        nch = (pf_nkb(qb, p0, m_rows) + cb - 1) / cb;
+        if (idx < nch) {
+            chunk = idx;
+            break;
+        }
+        idx -= nch;
+    }
     const int h = blockIdx.y;
     const int kvh = h / (heads / kv_heads);
     const int q_first = qb * QM;
@@ -250,6 +274,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
 
     const int kend = p0 + min(q_first + QM, m_rows);  // keys [0, kend)
     const int nkb = (kend + KB - 1) / KB;
+    const int kb0 = chunk * cb, kb1 = min(kb0 + cb, nkb);  // this workgroup's key blocks
     const __half* kc = k_cache + (size_t)kvh * max_seq * D;
     const __half* vc = v_cache + (size_t)kvh * max_seq * D;
     // staging: thread t moves 16 B (8 dims) of key rows t / 16 + 16 i, chunk t % 16
@@ -302,12 +327,12 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
     for (int j = 0; j < 8; ++j) o[j] = f4{0.f, 0.f, 0.f, 0.f};
     const int qpos0 = p0 + q_first + 16 * w + 4 * fq;  // position of accumulator row r: qpos0 + r
 
-    gload(0);
-    for (int kb = 0; kb < nkb; ++kb) {
+    gload(kb0);
+    for (int kb = kb0; kb < kb1; ++kb) {
         __syncthreads();  // every wave finished reading the previous block
         lstore();
         __syncthreads();
-        if (kb + 1 < nkb) gload(kb + 1);
+        if (kb + 1 < kb1) gload(kb + 1);
 
         f4 s[4];
 #pragma unroll
@@ -339,13 +364,16 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
         float alpha[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float m_new = fmaxf(m_run[r], mx[r]);  // finite: key 0 is visible to every row
-            alpha[r] = expf(m_run[r] - m_new);
+            // a chunk that starts after a row's position masks all of its keys for that
+            // row: m stays -inf, p = 0 (chunk 0 holds key 0, visible to every row)
+            const float m_new = fmaxf(m_run[r], mx[r]);
+            const float m_use = m_new == -INFINITY ? 0.f : m_new;
+            alpha[r] = expf(m_run[r] - m_use);
             m_run[r] = m_new;
             float ps = 0.f;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float pv = expf(s[j][r] - m_new);
+                const float pv = expf(s[j][r] - m_use);
                 s[j][r] = pv;
                 ps += pv;
             }
@@ -388,6 +416,20 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
         __builtin_amdgcn_wave_barrier();  // P image is rewritten next block
     }
 
+    if (nch > 1) {  // partial: unnormalised O rows, m, l of this chunk
+        float* part = ws + ((size_t)(h * nqb + qb) * maxc + chunk) * kPartFloats;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int lr = 16 * w + 4 * fq + r;
+#pragma unroll
+            for (int jt = 0; jt < 8; ++jt) part[lr * D + 16 * jt + fr] = o[jt][r];
+            if (fr == 0) {
+                part[QM * D + lr] = m_run[r];
+                part[QM * D + QM + lr] = l_run[r];
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int row = q_first + 16 * w + 4 * fq + r;
@@ -404,6 +446,53 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
             } else {
                 out[idx] = v;
             }
+        }
+    }
+}
+
+// grid (nqb, heads), block 256: the chunks of a split query block, combined in chunk
+// order: M = max m_c, L = sum l_c e^(m_c - M), O = sum O_c e^(m_c - M) / L. Thread t:
+// row t / 4, dims 32 (t % 4) .. + 32.
+__global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const float* ws, int maxc, int cb, int m_rows,
+                                                                      int p0, float* out, _Float16* out_hi,
+                                                                      _Float16* out_lo, int ldo) {
+    const int qb = blockIdx.x, h = blockIdx.y, nqb = gridDim.x;
+    const int nch = (pf_nkb(qb, p0, m_rows) + cb - 1) / cb;
+    if (nch <= 1) return;  // written directly by the attention kernel
+    const int lr = threadIdx.x >> 2, d0 = (threadIdx.x & 3) * 32;
+    const int row = qb * QM + lr;
+    if (row >= m_rows) return;
+    const float* base = ws + (size_t)(h * nqb + qb) * maxc * kPartFloats;
+    float M = -INFINITY;
+    for (int c = 0; c < nch; ++c) M = fmaxf(M, base[(size_t)c * kPartFloats + QM * D + lr]);
+    float L = 0.f, acc[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc[i] = 0.f;
+    for (int c = 0; c < nch; ++c) {
+        const float* part = base + (size_t)c * kPartFloats;
+        const float wgt = expf(part[QM * D + lr] - M);  // 0 for a fully masked chunk (m = -inf)
+        L += part[QM * D + QM + lr] * wgt;
+        const float4* o4 = reinterpret_cast<const float4*>(part + lr * D + d0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 v = o4[i];
+            acc[4 * i] += v.x * wgt;
+            acc[4 * i + 1] += v.y * wgt;
+            acc[4 * i + 2] += v.z * wgt;
+            acc[4 * i + 3] += v.w * wgt;
+        }
+    }
+    const float inv = 1.0f / L;
+    const size_t idx = (size_t)row * ldo + (size_t)h * D + d0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const float v = acc[i] * inv;
+        if (out_hi) {
+            const _Float16 hi = (_Float16)v;
+            out_hi[idx + i] = hi;
+            if (out_lo) out_lo[idx + i] = (_Float16)(v - (float)hi);
+        } else {
+            out[idx + i] = v;
         }
     }
 }
@@ -440,15 +529,33 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(rope_kv_prefill_kernel<__half>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (__half*)a.k_cache, (__half*)a.v_cache, a.max_seq);
         if (a.mfma_planes) {
-            const dim3 gm((a.m + QM - 1) / QM, a.heads);
+            // split keys: chunks of cb key blocks, cb sized for ~1024 workgroups
+            const int nqb = (a.m + QM - 1) / QM;
+            int blocks = 0, max_nkb = 0;
+            for (int qb = 0; qb < nqb; ++qb) {
+                blocks += pf_nkb(qb, a.p0, a.m);
+                max_nkb = std::max(max_nkb, pf_nkb(qb, a.p0, a.m));
+            }
+            int cb = a.split_ws ? std::max(2, (blocks * a.heads + 1023) / 1024) : max_nkb;
+            int maxc = (max_nkb + cb - 1) / cb;
+            if (a.split_ws && (size_t)a.heads * nqb * maxc * kPartFloats > a.split_ws_floats) {
+                cb = max_nkb;  // no room: one chunk per query block
+                maxc = 1;
+            }
+            int grid = 0;
+            for (int qb = 0; qb < nqb; ++qb) grid += (pf_nkb(qb, a.p0, a.m) + cb - 1) / cb;
+            const dim3 gm(grid, a.heads);
             if (a.mfma_planes == 2)
                 hipLaunchKernelGGL(attn_prefill_mfma_kernel<2>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
                                    a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
-                                   a.out, a.out_hi, a.out_lo, a.heads * D);
+                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc);
             else
                 hipLaunchKernelGGL(attn_prefill_mfma_kernel<1>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
                                    a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
-                                   a.out, a.out_hi, a.out_lo, a.heads * D);
+                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc);
+            if (maxc > 1)
+                hipLaunchKernelGGL(attn_prefill_merge_kernel, dim3(nqb, a.heads), dim3(kThreads), 0, s, a.split_ws,
+                                   maxc, cb, a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D);
         } else {
             hipLaunchKernelGGL(attn_prefill_kernel<__half>, ga, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0, a.heads,
                                a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq, a.out,
