@@ -214,55 +214,70 @@ __global__ __launch_bounds__(kThreads) void gemm2_kernel(Gemm2Args a) {
 
 // RMSNorm (optional) + split of fp32 rows into fp16 planes: one workgroup per row.
 // v = x * rsqrt(mean(x^2) + eps) * gamma (the reference's order, modeling_llama.py:
-// 112-117); hi = fp16(v), lo = fp16(v - hi).
+// 112-117); hi = fp16(v), lo = fp16(v - hi). The row stays in registers (NPT float4s
+// per thread, k <= NPT * 1024): x and the slab slices are read once, x written once.
+template <int NPT>
 __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx, int k, const void* gamma,
                                                              int g_dtype, float eps, _Float16* hi, _Float16* lo,
                                                              int ldh, const float* slab, int ksplit, int m) {
     __shared__ float red[16];
     float* xr = x + (size_t)blockIdx.x * ldx;
     const int k4 = k / 4;
+    float4 v[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+        const int j = threadIdx.x + i * kThreads;
+        v[i] = j < k4 ? reinterpret_cast<const float4*>(xr)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (slab) {  // split-K combine: x += slice 0 + slice 1 + ... (fixed order), written back
-        for (int j = threadIdx.x; j < k4; j += kThreads) {
-            float4 v = reinterpret_cast<const float4*>(xr)[j];
-            for (int s = 0; s < ksplit; ++s) {
-                const float4 p = reinterpret_cast<const float4*>(slab + ((size_t)s * m + blockIdx.x) * ldx)[j];
-                v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+        for (int s = 0; s < ksplit; ++s) {
+            const float4* sl = reinterpret_cast<const float4*>(slab + ((size_t)s * m + blockIdx.x) * ldx);
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                const int j = threadIdx.x + i * kThreads;
+                if (j < k4) {
+                    const float4 p = sl[j];
+                    v[i].x += p.x; v[i].y += p.y; v[i].z += p.z; v[i].w += p.w;
+                }
             }
-            reinterpret_cast<float4*>(xr)[j] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int j = threadIdx.x + i * kThreads;
+            if (j < k4) reinterpret_cast<float4*>(xr)[j] = v[i];
         }
         if (!hi) return;
-        __syncthreads();
     }
     float rstd = 1.f;
     if (gamma) {
         float ss = 0.f;
-        for (int j = threadIdx.x; j < k4; j += kThreads) {
-            const float4 v = reinterpret_cast<const float4*>(xr)[j];
-            ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-        }
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) ss += v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
         ss = block_sum(ss, red);
         rstd = 1.0f / sqrtf(ss / (float)k + eps);
     }
     if (!hi) return;
     _Float16* hr = hi + (size_t)blockIdx.x * ldh;
     _Float16* lr = lo ? lo + (size_t)blockIdx.x * ldh : nullptr;
-    for (int j = threadIdx.x; j < k4; j += kThreads) {
-        const float4 x4 = reinterpret_cast<const float4*>(xr)[j];
-        float v[4] = {x4.x, x4.y, x4.z, x4.w};
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+        const int j = threadIdx.x + i * kThreads;
+        if (j >= k4) continue;
+        float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
         if (gamma) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float g = g_dtype == LLMI_F16 ? __half2float(static_cast<const __half*>(gamma)[4 * j + e])
-                                                    : static_cast<const float*>(gamma)[4 * j + e];
-                v[e] = (v[e] * rstd) * g;
+            for (int q = 0; q < 4; ++q) {
+                const float g = g_dtype == LLMI_F16 ? __half2float(static_cast<const __half*>(gamma)[4 * j + q])
+                                                    : static_cast<const float*>(gamma)[4 * j + q];
+                e[q] = (e[q] * rstd) * g;
             }
         }
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 h, l;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            h[e] = (_Float16)v[e];
-            l[e] = (_Float16)(v[e] - (float)h[e]);
+        for (int q = 0; q < 4; ++q) {
+            h[q] = (_Float16)e[q];
+            l[q] = (_Float16)(e[q] - (float)h[q]);
         }
         reinterpret_cast<h4*>(hr)[j] = h;
         if (lr) reinterpret_cast<h4*>(lr)[j] = l;
@@ -341,8 +356,18 @@ int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_
     LLMI_REQUIRE(x && (hi || slab) && m > 0 && k > 0 && k % 4 == 0 && ldx % 4 == 0 && ldh % 4 == 0,
                  "rows_split: bad arguments");
     LLMI_REQUIRE(!slab || (ksplit >= 1 && ldx == k), "rows_split: slab rows must be dense (ldx == k)");
-    hipLaunchKernelGGL(rows_split_kernel, dim3(m), dim3(kThreads), 0, s, x, ldx, k, gamma, g_dtype, eps, hi, lo, ldh,
-                       slab, ksplit, m);
+    LLMI_REQUIRE(k <= 8 * 4 * kThreads, "rows_split: rows longer than 8192 are not supported");
+    const int npt = (k / 4 + kThreads - 1) / kThreads;
+#define RS_LAUNCH(N) \
+    hipLaunchKernelGGL(rows_split_kernel<N>, dim3(m), dim3(kThreads), 0, s, x, ldx, k, gamma, g_dtype, eps, hi, lo, ldh, \
+                       slab, ksplit, m)
+    if (npt <= 4)
+        RS_LAUNCH(4);
+    else if (npt <= 5)
+        RS_LAUNCH(5);
+    else
+        RS_LAUNCH(8);
+#undef RS_LAUNCH
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }

@@ -36,39 +36,59 @@ __device__ __forceinline__ float load_c(const float* p) { return *p; }
 
 // grid (M), block 256: row m of qkv [M, (heads + 2 kv) * D]; with qkv2 (the second
 // K slice of the qkv GEMM) each element is qkv + qkv2 first, and the summed, rotated q
-// is what stays in qkv
+// is what stays in qkv. Thread work item e: head e / 16, dims 4 (e % 16) .. + 3 and
+// their RoPE partners + 64, as float4s (the pair expression is the decode kernel's).
 template <typename KT>
 __global__ void rope_kv_prefill_kernel(float* qkv, const float* qkv2, int ld, int p0, int heads, int kv_heads,
                                        const float* rope_tab, KT* k_cache, KT* v_cache, int max_seq) {
     const int m = blockIdx.x, pos = p0 + m;
     float* row = qkv + (size_t)m * ld;
     const float* row2 = qkv2 ? qkv2 + (size_t)m * ld : nullptr;
-    const float2* cs = reinterpret_cast<const float2*>(rope_tab) + (size_t)pos * (D / 2);
-    // q heads then k heads: pairs (i, i + D/2), same expression as attn_decode_kernel
-    for (int e = threadIdx.x; e < (heads + kv_heads) * (D / 2); e += blockDim.x) {
-        const int hh = e / (D / 2), i = e % (D / 2);
-        const float c = cs[i].x, s = cs[i].y;
+    const float4* cs4 = reinterpret_cast<const float4*>(rope_tab + (size_t)pos * D);  // (cos, sin) pairs
+    for (int e = threadIdx.x; e < (heads + kv_heads) * (D / 8); e += blockDim.x) {
+        const int hh = e / (D / 8), i = 4 * (e % (D / 8));
         float* p = row + (size_t)hh * D;
-        float x0 = p[i], x1 = p[i + D / 2];
+        float4 x0 = *reinterpret_cast<const float4*>(p + i), x1 = *reinterpret_cast<const float4*>(p + i + D / 2);
         if (row2) {
-            x0 += row2[(size_t)hh * D + i];
-            x1 += row2[(size_t)hh * D + i + D / 2];
+            const float* p2 = row2 + (size_t)hh * D;
+            const float4 y0 = *reinterpret_cast<const float4*>(p2 + i), y1 = *reinterpret_cast<const float4*>(p2 + i + D / 2);
+            x0.x += y0.x; x0.y += y0.y; x0.z += y0.z; x0.w += y0.w;
+            x1.x += y1.x; x1.y += y1.y; x1.z += y1.z; x1.w += y1.w;
         }
-        const float r0 = x0 * c - x1 * s, r1 = x1 * c + x0 * s;
+        const float4 c01 = cs4[i / 2], c23 = cs4[i / 2 + 1];  // (c, s) of dims i .. i + 3
+        const float c[4] = {c01.x, c01.z, c23.x, c23.z}, sn[4] = {c01.y, c01.w, c23.y, c23.w};
+        const float a0[4] = {x0.x, x0.y, x0.z, x0.w}, a1[4] = {x1.x, x1.y, x1.z, x1.w};
+        float r0[4], r1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            r0[j] = a0[j] * c[j] - a1[j] * sn[j];
+            r1[j] = a1[j] * c[j] + a0[j] * sn[j];
+        }
         if (hh < heads) {
-            p[i] = r0;
-            p[i + D / 2] = r1;
+            *reinterpret_cast<float4*>(p + i) = make_float4(r0[0], r0[1], r0[2], r0[3]);
+            *reinterpret_cast<float4*>(p + i + D / 2) = make_float4(r1[0], r1[1], r1[2], r1[3]);
         } else {
             KT* kc = k_cache + ((size_t)(hh - heads) * max_seq + pos) * D;
-            store_c(kc + i, r0);
-            store_c(kc + i + D / 2, r1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                store_c(kc + i + j, r0[j]);
+                store_c(kc + i + j + D / 2, r1[j]);
+            }
         }
     }
     const size_t vo = (size_t)(heads + kv_heads) * D;
-    for (int e = threadIdx.x; e < kv_heads * D; e += blockDim.x) {
-        const int hh = e / D, d = e % D;
-        const float v = row2 ? row[vo + e] + row2[vo + e] : row[vo + e];
-        store_c(v_cache + ((size_t)hh * max_seq + pos) * D + d, v);
+    for (int e = threadIdx.x; e < kv_heads * (D / 4); e += blockDim.x) {
+        const int hh = e / (D / 4), d = 4 * (e % (D / 4));
+        float4 v = *reinterpret_cast<const float4*>(row + vo + 4 * e);
+        if (row2) {
+            const float4 y = *reinterpret_cast<const float4*>(row2 + vo + 4 * e);
+            v.x += y.x; v.y += y.y; v.z += y.z; v.w += y.w;
+        }
+        KT* vc = v_cache + ((size_t)hh * max_seq + pos) * D + d;
+        store_c(vc, v.x);
+        store_c(vc + 1, v.y);
+        store_c(vc + 2, v.z);
+        store_c(vc + 3, v.w);
     }
 }
 
@@ -213,7 +233,7 @@ __device__ __forceinline__ int vswz(int d) { return (d ^ (d >> 3)) & 7; }  // Vt
 constexpr int KB = 64;  // keys per block
 
 // Split keys: the causal range of query block qb (key blocks [0, nkb(qb))) is cut into
-// chunks of cb key blocks, one workgroup each, so the longest query blocks no longer set
+// chunks of cb key blocks, one workgroup each (~512: two fit per CU), so the longest query blocks no longer set
 // the kernel's critical path (8 dependent key blocks at M = 512). A query block with one
 // chunk writes its output directly; otherwise every chunk writes its unnormalised
 // (O, m, l) to ws[head][qb][chunk] and attn_prefill_merge_kernel combines them in
@@ -451,48 +471,64 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
 }
 
 // grid (nqb, heads), block 256: the chunks of a split query block, combined in chunk
-// order: M = max m_c, L = sum l_c e^(m_c - M), O = sum O_c e^(m_c - M) / L. Thread t:
-// row t / 4, dims 32 (t % 4) .. + 32.
+// order: M = max m_c, L = sum l_c e^(m_c - M), O = sum O_c e^(m_c - M) / L. Four passes
+// of 16 rows; thread t: row 16 pass + t / 16, dims 8 (t % 16) .. + 8, so 16 lanes cover a
+// row with 16-B loads and stores. Every chunk's loads are issued before any is used
+// (MAXC slots, clamped chunk index, unused slots weighted 0): one memory round trip.
+template <int MAXC>
 __global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const float* ws, int maxc, int cb, int m_rows,
                                                                       int p0, float* out, _Float16* out_hi,
                                                                       _Float16* out_lo, int ldo) {
     const int qb = blockIdx.x, h = blockIdx.y, nqb = gridDim.x;
     const int nch = (pf_nkb(qb, p0, m_rows) + cb - 1) / cb;
     if (nch <= 1) return;  // written directly by the attention kernel
-    const int lr = threadIdx.x >> 2, d0 = (threadIdx.x & 3) * 32;
-    const int row = qb * QM + lr;
-    if (row >= m_rows) return;
     const float* base = ws + (size_t)(h * nqb + qb) * maxc * kPartFloats;
-    float M = -INFINITY;
-    for (int c = 0; c < nch; ++c) M = fmaxf(M, base[(size_t)c * kPartFloats + QM * D + lr]);
-    float L = 0.f, acc[32];
+    const int d0 = (threadIdx.x & 15) * 8;
+    for (int pass = 0; pass < QM / 16; ++pass) {
+        const int lr = pass * 16 + (threadIdx.x >> 4);
+        const int row = qb * QM + lr;
+        if (row >= m_rows) break;
+        float mc[MAXC], lc[MAXC];
+        float4 oc[MAXC][2];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) acc[i] = 0.f;
-    for (int c = 0; c < nch; ++c) {
-        const float* part = base + (size_t)c * kPartFloats;
-        const float wgt = expf(part[QM * D + lr] - M);  // 0 for a fully masked chunk (m = -inf)
-        L += part[QM * D + QM + lr] * wgt;
-        const float4* o4 = reinterpret_cast<const float4*>(part + lr * D + d0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float4 v = o4[i];
-            acc[4 * i] += v.x * wgt;
-            acc[4 * i + 1] += v.y * wgt;
-            acc[4 * i + 2] += v.z * wgt;
-            acc[4 * i + 3] += v.w * wgt;
+        for (int c = 0; c < MAXC; ++c) {
+            const float* part = base + (size_t)min(c, nch - 1) * kPartFloats;
+            mc[c] = part[QM * D + lr];
+            lc[c] = part[QM * D + QM + lr];
+            const float4* o4 = reinterpret_cast<const float4*>(part + lr * D + d0);
+            oc[c][0] = o4[0];
+            oc[c][1] = o4[1];
         }
-    }
-    const float inv = 1.0f / L;
-    const size_t idx = (size_t)row * ldo + (size_t)h * D + d0;
+        float M = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        const float v = acc[i] * inv;
+        for (int c = 0; c < MAXC; ++c) M = fmaxf(M, mc[c]);  // clamped slots repeat a real chunk
+        float L = 0.f, acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const float wgt = c < nch ? expf(mc[c] - M) : 0.f;  // 0 for a fully masked chunk (m = -inf)
+            L += lc[c] * wgt;
+            const float v[8] = {oc[c][0].x, oc[c][0].y, oc[c][0].z, oc[c][0].w,
+                                oc[c][1].x, oc[c][1].y, oc[c][1].z, oc[c][1].w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] += v[i] * wgt;
+        }
+        const float inv = 1.0f / L;
+        const size_t idx = (size_t)row * ldo + (size_t)h * D + d0;
         if (out_hi) {
-            const _Float16 hi = (_Float16)v;
-            out_hi[idx + i] = hi;
-            if (out_lo) out_lo[idx + i] = (_Float16)(v - (float)hi);
+            h8 hv, lv;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float v = acc[i] * inv;
+                hv[i] = (_Float16)v;
+                lv[i] = (_Float16)(v - (float)hv[i]);
+            }
+            *reinterpret_cast<h8*>(out_hi + idx) = hv;
+            if (out_lo) *reinterpret_cast<h8*>(out_lo + idx) = lv;
         } else {
-            out[idx + i] = v;
+            *reinterpret_cast<float4*>(out + idx) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+            *reinterpret_cast<float4*>(out + idx + 4) = make_float4(acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv);
         }
     }
 }
@@ -529,16 +565,17 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(rope_kv_prefill_kernel<__half>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (__half*)a.k_cache, (__half*)a.v_cache, a.max_seq);
         if (a.mfma_planes) {
-            // split keys: chunks of cb key blocks, cb sized for ~1024 workgroups
+            // split keys: chunks of cb key blocks
             const int nqb = (a.m + QM - 1) / QM;
             int blocks = 0, max_nkb = 0;
             for (int qb = 0; qb < nqb; ++qb) {
                 blocks += pf_nkb(qb, a.p0, a.m);
                 max_nkb = std::max(max_nkb, pf_nkb(qb, a.p0, a.m));
             }
-            int cb = a.split_ws ? std::max(2, (blocks * a.heads + 1023) / 1024) : max_nkb;
+            // (189-214 VGPRs: two workgroups per CU, so ~512 workgroups run in one round)
+            int cb = a.split_ws ? std::max(2, (blocks * a.heads + 511) / 512) : max_nkb;
             int maxc = (max_nkb + cb - 1) / cb;
-            if (a.split_ws && (size_t)a.heads * nqb * maxc * kPartFloats > a.split_ws_floats) {
+            if (a.split_ws && (maxc > 8 || (size_t)a.heads * nqb * maxc * kPartFloats > a.split_ws_floats)) {
                 cb = max_nkb;  // no room: one chunk per query block
                 maxc = 1;
             }
@@ -553,9 +590,18 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
                 hipLaunchKernelGGL(attn_prefill_mfma_kernel<1>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
                                    a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
                                    a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc);
-            if (maxc > 1)
-                hipLaunchKernelGGL(attn_prefill_merge_kernel, dim3(nqb, a.heads), dim3(kThreads), 0, s, a.split_ws,
-                                   maxc, cb, a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D);
+            if (maxc > 1) {
+#define PF_MERGE(C)                                                                                              \
+    hipLaunchKernelGGL(attn_prefill_merge_kernel<C>, dim3(nqb, a.heads), dim3(kThreads), 0, s, a.split_ws, maxc, cb, \
+                       a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D)
+                if (maxc <= 2)
+                    PF_MERGE(2);
+                else if (maxc <= 4)
+                    PF_MERGE(4);
+                else
+                    PF_MERGE(8);
+#undef PF_MERGE
+            }
         } else {
             hipLaunchKernelGGL(attn_prefill_kernel<__half>, ga, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0, a.heads,
                                a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq, a.out,
