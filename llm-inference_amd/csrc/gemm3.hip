@@ -48,10 +48,11 @@ constexpr int kTile = 256;           // BM = BN
 constexpr int kK = 64;               // K per tile step (128-B LDS rows)
 constexpr int kHalf = 128 * 128;     // one half-image: 128 rows x 128 B
 constexpr int kBuf = 4 * kHalf;      // A0 A1 B0 B1
-constexpr int kLds = 2 * kBuf;       // 128 KB
+constexpr int kEpiRowB = 272;        // gate_up epilogue image: 128 halves + 16 B pad per row
+constexpr int kLds = 2 * kBuf > 2 * kTile * kEpiRowB ? 2 * kBuf : 2 * kTile * kEpiRowB;  // 136 KB
 
 #ifndef LLMI_G3_EXP
-#define LLMI_G3_EXP 0  // timing experiments only: 1 no DMA in the loop, 2 no LDS reads, 3 no DMA waits
+#define LLMI_G3_EXP 0  // timing experiments only: 1 no DMA in the loop, 2 no LDS reads, 3 no DMA waits, 4 no stores
 #endif
 #ifndef LLMI_G3_LGKM_EARLY
 #define LLMI_G3_LGKM_EARLY 0
@@ -250,8 +251,45 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
     }
     if (wr == 0) bar();  // equal barrier counts
 
+#if LLMI_G3_EXP == 4
+    if (KT > 0) return;  // timing experiment: no epilogue stores
+#endif
     // epilogue: acc[qa][qb][i][j] register e is tile row qa*128 + wr*64 + 16 i + 4 fq + e,
     // tile column qb*128 + wc*32 + 16 j + fr (SILU: qb 0 gate, qb 1 its up column)
+    if (EPI == EPI_SILU_MUL && a.y_hi) {
+        // fp16 planes through LDS (the K loop's reads and DMA are all retired here), then
+        // 16-B stores: 16 lanes per 256-B row instead of 2-B stores 4 rows per instruction
+        // (measured store-issue-bound: 7-10 us of a 110 us gate_up). Rows padded to 272 B:
+        // the accumulator rows 4 apart land 16 banks apart.
+        char* img = lds;
+#pragma unroll
+        for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int row = qa * 128 + wr * 64 + 16 * i + 4 * fq + e, col = wc * 32 + 16 * j + fr;
+                        const float v = silu3(acc[qa][0][i][j][e]) * acc[qa][1][i][j][e];
+                        const _Float16 hi = (_Float16)v;
+                        *reinterpret_cast<_Float16*>(img + row * kEpiRowB + col * 2) = hi;
+                        if (a.y_lo)
+                            *reinterpret_cast<_Float16*>(img + (kTile + row) * kEpiRowB + col * 2) =
+                                (_Float16)(v - (float)hi);
+                    }
+        __syncthreads();
+        const int planes = a.y_lo ? 2 : 1;
+        for (int c = t; c < planes * kTile * 16; c += kT) {
+            const int pl = c / (kTile * 16), row = (c >> 4) & (kTile - 1), ch = c & 15;
+            const int m = m0 + row;
+            if (m >= a.m) continue;
+            const h8v v = *reinterpret_cast<const h8v*>(img + (pl * kTile + row) * kEpiRowB + ch * 16);
+            _Float16* dst = (pl ? a.y_lo : a.y_hi) + (size_t)m * a.ldy + ct * 128 + ch * 8;
+            *reinterpret_cast<h8v*>(dst) = v;
+        }
+        return;
+    }
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
@@ -325,6 +363,10 @@ int gemm3_launch(Gemm2Args a, hipStream_t s) {
                  "gemm3: A planes must be 16-B aligned with lda % 8 == 0");
     LLMI_REQUIRE((reinterpret_cast<uintptr_t>(a.w) & 15) == 0 && a.k % 8 == 0, "gemm3: W must be 16-B aligned");
     LLMI_REQUIRE(a.epi != EPI_SILU_MUL || a.pair_off == a.n / 2, "gemm3: gate_up pair offset must be N / 2");
+    LLMI_REQUIRE(a.epi != EPI_SILU_MUL || !a.y_hi ||
+                     (a.ldy % 8 == 0 && (reinterpret_cast<uintptr_t>(a.y_hi) & 15) == 0 &&
+                      (!a.y_lo || (reinterpret_cast<uintptr_t>(a.y_lo) & 15) == 0)),
+                 "gemm3: fp16 output planes must be 16-B aligned with ldy % 8 == 0");
     const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
     a.n_tiles = ncols / ((a.epi == EPI_SILU_MUL) ? 128 : kTile);
     const int grid = ((a.m + kTile - 1) / kTile) * a.n_tiles * a.ksplit;
