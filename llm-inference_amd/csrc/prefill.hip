@@ -436,36 +436,59 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
         __builtin_amdgcn_wave_barrier();  // P image is rewritten next block
     }
 
+    // epilogue through LDS (K/V/P images are free now): the O rows -- unnormalised for a
+    // partial, divided by l for a direct output -- as a padded fp32 image [64][132], then
+    // 16-B stores, 32 lanes per row (scalar stores spanned 4 rows per instruction)
+    __syncthreads();
+    float* img = reinterpret_cast<float*>(smem);
+    constexpr int kIs = D + 4;  // row stride: rows 4 apart land 16 banks apart
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int lr = 16 * w + 4 * fq + r;
+        const float sc = nch > 1 ? 1.f : 1.0f / l_run[r];
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) img[lr * kIs + 16 * jt + fr] = o[jt][r] * sc;
+    }
     if (nch > 1) {  // partial: unnormalised O rows, m, l of this chunk
         float* part = ws + ((size_t)(h * nqb + qb) * maxc + chunk) * kPartFloats;
+        if (fr == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int lr = 16 * w + 4 * fq + r;
-#pragma unroll
-            for (int jt = 0; jt < 8; ++jt) part[lr * D + 16 * jt + fr] = o[jt][r];
-            if (fr == 0) {
+            for (int r = 0; r < 4; ++r) {
+                const int lr = 16 * w + 4 * fq + r;
                 part[QM * D + lr] = m_run[r];
                 part[QM * D + QM + lr] = l_run[r];
             }
         }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < QM * D / 4 / kThreads; ++i) {
+            const int f = i * kThreads + t, lr = f >> 5, c4 = f & 31;
+            reinterpret_cast<float4*>(part)[f] = *reinterpret_cast<const float4*>(img + lr * kIs + 4 * c4);
+        }
         return;
     }
+    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = q_first + 16 * w + 4 * fq + r;
+    for (int i = 0; i < QM * D / 8 / kThreads; ++i) {
+        const int f = i * kThreads + t, lr = f >> 4, c8 = f & 15;
+        const int row = q_first + lr;
         if (row >= m_rows) continue;
-        const float inv = 1.0f / l_run[r];
+        const float4 x0 = *reinterpret_cast<const float4*>(img + lr * kIs + 8 * c8);
+        const float4 x1 = *reinterpret_cast<const float4*>(img + lr * kIs + 8 * c8 + 4);
+        const size_t idx = (size_t)row * ldo + (size_t)h * D + 8 * c8;
+        if (out_hi) {
+            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            h8 hv, lv;
 #pragma unroll
-        for (int jt = 0; jt < 8; ++jt) {
-            const size_t idx = (size_t)row * ldo + (size_t)h * D + 16 * jt + fr;
-            const float v = o[jt][r] * inv;
-            if (out_hi) {
-                const _Float16 hi = (_Float16)v;
-                out_hi[idx] = hi;
-                if (out_lo) out_lo[idx] = (_Float16)(v - (float)hi);
-            } else {
-                out[idx] = v;
+            for (int e = 0; e < 8; ++e) {
+                hv[e] = (_Float16)v[e];
+                lv[e] = (_Float16)(v[e] - (float)hv[e]);
             }
+            *reinterpret_cast<h8*>(out_hi + idx) = hv;
+            if (out_lo) *reinterpret_cast<h8*>(out_lo + idx) = lv;
+        } else {
+            *reinterpret_cast<float4*>(out + idx) = x0;
+            *reinterpret_cast<float4*>(out + idx + 4) = x1;
         }
     }
 }
