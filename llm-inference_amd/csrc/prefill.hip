@@ -272,23 +272,17 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
     const int q_first = qb * QM;
     const float qscale = 1.0f / sqrtf((float)D);
 
-    // Q fragments: row q_first + 16 w + fr, dims 32 ks + 8 fq + [0, 8)
+    // Q fragments: row q_first + 16 w + fr, dims 32 ks + 8 fq + [0, 8). The raw loads go
+    // out first, then the first K/V block's (below), then the conversion: one round trip
     h8 qa[P][4];
+    float4 qraw[4][2];
     {
         const int qrow = min(q_first + 16 * w + fr, m_rows - 1);
         const float* qp = qkv + (size_t)qrow * ld + (size_t)h * D;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-            const float4 a = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq);
-            const float4 b = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq + 4);
-            const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float x = v[e] * qscale;
-                const _Float16 hi = (_Float16)x;
-                qa[0][ks][e] = hi;
-                if (P == 2) qa[P - 1][ks][e] = (_Float16)(x - (float)hi);
-            }
+            qraw[ks][0] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq);
+            qraw[ks][1] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq + 4);
         }
     }
 
@@ -348,6 +342,18 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
     const int qpos0 = p0 + q_first + 16 * w + 4 * fq;  // position of accumulator row r: qpos0 + r
 
     gload(kb0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const float v[8] = {qraw[ks][0].x, qraw[ks][0].y, qraw[ks][0].z, qraw[ks][0].w,
+                            qraw[ks][1].x, qraw[ks][1].y, qraw[ks][1].z, qraw[ks][1].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float x = v[e] * qscale;
+            const _Float16 hi = (_Float16)x;
+            qa[0][ks][e] = hi;
+            if (P == 2) qa[P - 1][ks][e] = (_Float16)(x - (float)hi);
+        }
+    }
     for (int kb = kb0; kb < kb1; ++kb) {
         __syncthreads();  // every wave finished reading the previous block
         lstore();
