@@ -41,7 +41,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_pf -o pf --outpu
 find /tmp/prof_pf -name '*kernel_stats.csv' -exec cp {} $OUT/prefill_kernel_stats_$TAG.csv \;
 echo "[$(date +%T)] pmc mfma (prefill GEMM)"
 rm -rf /tmp/pmc_m
-timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE --kernel-include-regex 'gemm2?_kernel|attn_prefill' -d /tmp/pmc_m -o pmc --output-format csv -- python3 tools/prefill_probe.py 512 1 > $OUT/pmc_mfma_$TAG.log 2>&1 || { echo "pmc mfma failed $?"; tail -20 $OUT/pmc_mfma_$TAG.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE --kernel-include-regex 'gemm[23]?_kernel|attn_prefill' -d /tmp/pmc_m -o pmc --output-format csv -- python3 tools/prefill_probe.py 512 1 > $OUT/pmc_mfma_$TAG.log 2>&1 || { echo "pmc mfma failed $?"; tail -20 $OUT/pmc_mfma_$TAG.log; exit 1; }
 find /tmp/pmc_m -name '*counter_collection.csv' -exec cp {} $OUT/pmc_mfma_$TAG.csv \;
 echo "[$(date +%T)] counters available"
 timeout -k 10 120 rocprofv3 -L > $OUT/rocprof_counters_$TAG.txt 2>&1 || true
