@@ -145,13 +145,13 @@ def attention_prefill(q: np.ndarray, k_cache: np.ndarray, v_cache: np.ndarray, p
     group = heads // k_cache.shape[0]
     k = np.repeat(k_cache[:, :ctx].astype(np.float32), group, axis=0)
     v = np.repeat(v_cache[:, :ctx].astype(np.float32), group, axis=0)
-    s = np.einsum("mhd,hjd->hmj", q.astype(np.float32), k) / np.float32(math.sqrt(d))
+    s = np.matmul(q.astype(np.float32).transpose(1, 0, 2), k.transpose(0, 2, 1)) / np.float32(math.sqrt(d))
     allowed = np.arange(ctx)[None, :] <= (p0 + np.arange(m))[:, None]
     s = np.where(allowed[None], s, np.float32(-np.inf))
     s = s - s.max(axis=-1, keepdims=True)
     pr = np.exp(s)
     pr = pr / pr.sum(axis=-1, keepdims=True)
-    return np.einsum("hmj,hjd->mhd", pr.astype(np.float32), v).astype(np.float32)
+    return np.matmul(pr.astype(np.float32), v).transpose(1, 0, 2).astype(np.float32)
 
 
 def argmax_first(logits: np.ndarray) -> int:
@@ -229,14 +229,45 @@ class ModelWeights:
     layers: List[LayerWeights]
 
 
+# In-process memo of generated weights (test-suite time: a 7B-width PRNG model takes ~30 s
+# of numpy): the embedding per (seed, vocab, hidden) -- every TP rank shares it -- and
+# whole unsharded models per (config without max_seq, seed, int8), at most two kept.
+# The arrays are shared, so they are made read-only.
+_EMBED_MEMO: Dict[tuple, np.ndarray] = {}
+_MODEL_MEMO: Dict[tuple, "ModelWeights"] = {}
+
+
+def _readonly(a: np.ndarray) -> np.ndarray:
+    a.setflags(write=False)
+    return a
+
+
 def make_model_weights(cfg: LlamaConfig, seed: int, int8: bool = False,
                        tp_rank: int = 0, tp_world: int = 1) -> ModelWeights:
+    key = (dataclasses.replace(cfg, max_seq=0), seed, int8)
+    if tp_world == 1 and key in _MODEL_MEMO:
+        return _MODEL_MEMO[key]
+    ek = (seed, cfg.vocab, cfg.hidden)
+    if ek not in _EMBED_MEMO:
+        _EMBED_MEMO[ek] = _readonly(prng.embed_fp16(seed, prng.GLOBAL_EMBED, cfg.vocab, cfg.hidden))
     vn = cfg.vocab // tp_world
-    return ModelWeights(
-        embed=prng.embed_fp16(seed, prng.GLOBAL_EMBED, cfg.vocab, cfg.hidden),
+    w = ModelWeights(
+        embed=_EMBED_MEMO[ek],
         lm_head=prng.linear_fp16(seed, prng.GLOBAL_LM_HEAD, vn, cfg.hidden, tp_rank * vn, 0, cfg.hidden),
         final_norm=prng.gamma_fp16(seed, prng.GLOBAL_FINAL_NORM, cfg.hidden),
         layers=[make_layer_weights(cfg, seed, l, int8, tp_rank, tp_world) for l in range(cfg.layers)])
+    if tp_world == 1:
+        for a in (w.lm_head, w.final_norm):
+            _readonly(a)
+        for lw in w.layers:
+            for f in dataclasses.fields(lw):
+                a = getattr(lw, f.name)
+                if isinstance(a, np.ndarray):
+                    _readonly(a)
+        if len(_MODEL_MEMO) >= 2:
+            _MODEL_MEMO.pop(next(iter(_MODEL_MEMO)))
+        _MODEL_MEMO[key] = w
+    return w
 
 
 # ------------------------------------------------------------------------- model

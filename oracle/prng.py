@@ -79,11 +79,24 @@ def _i24(bits: np.ndarray) -> np.ndarray:
 
 
 def _chunked(fn, rows, cols, row0, col0, ld, out_dtype, chunk_rows=None):
+    """Row blocks of ~256K elements (cache-sized temporaries) on a thread pool: numpy's
+    integer ufuncs release the GIL, and every element is a pure function of its index."""
+    import concurrent.futures as cf
+    import os
     out = np.empty((rows, cols), dtype=out_dtype)
-    step = chunk_rows or max(1, (1 << 22) // max(cols, 1))
-    for r in range(0, rows, step):
+    step = chunk_rows or max(1, (1 << 18) // max(cols, 1))
+
+    def block(r):
         n = min(step, rows - r)
         out[r:r + n] = fn(_index_grid(n, cols, row0 + r, col0, ld))
+
+    starts = range(0, rows, step)
+    if rows * cols < (1 << 20):
+        for r in starts:
+            block(r)
+    else:
+        with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+            list(ex.map(block, starts))
     return out
 
 
