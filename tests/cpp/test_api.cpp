@@ -3,6 +3,7 @@
 // running the MI355X kernels through libllmi.so. Prints one JSON line per check;
 // the layer-by-layer greedy decode prints its tokens for the pytest driver
 // (tests/test_gpu_cpp_api.py) to compare with the reference fixture.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -201,6 +202,54 @@ static void layer_decode(const std::vector<int>& prompt, int n_new, uint64_t see
     std::printf("{\"context_layer_tokens\": [");
     for (size_t i = 0; i < gen2.size(); ++i) std::printf("%s%d", i ? ", " : "", gen2[i]);
     std::printf("]}\n");
+
+    // ---- a ragged batch through LlamaContextDecoder (context_decoder.cpp:47-143 with bs > 1):
+    // three prefixes of the prompt (lengths n, n - 3, 4; no history) packed row after row,
+    // padding offsets and per-sequence causal masks from the launchers; the last row of each
+    // sequence -> final norm -> lm_head. The pytest driver compares every sequence with the
+    // oracle's prefill of that prefix alone.
+    {
+        const std::vector<int> lens = {n, n - 3, 4};
+        const int bs = (int)lens.size();
+        int tokens = 0, maxq = 0;
+        std::vector<int> rids;
+        for (int b = 0; b < bs; ++b) {
+            tokens += lens[b];
+            maxq = std::max(maxq, lens[b]);
+            for (int i = 0; i < lens[b]; ++i) rids.push_back(prompt[i]);
+        }
+        Dev<int> rid(rids), rhist(std::vector<int>(bs, 0)), rq(lens), rk(lens);
+        Dev<float> rx((size_t)tokens * H), ry((size_t)tokens * H), rkc((size_t)L * bs * kv * S * hd),
+            rvc((size_t)L * bs * kv * S * hd);
+        TensorWrapper<int> rid_t(GPU, INT32, {tokens}, rid.p), rhist_t(GPU, INT32, {bs}, rhist.p),
+            rq_t(GPU, INT32, {bs}, rq.p), rk_t(GPU, INT32, {bs}, rk.p);
+        TensorWrapper<float> rin(GPU, FP32, {tokens, H}, rx.p), rout(GPU, FP32, {tokens, H}, ry.p);
+        TensorWrapper<float> rkcache(GPU, FP32, {L, bs, kv, S, hd}, rkc.p), rvcache(GPU, FP32, {L, bs, kv, S, hd}, rvc.p);
+        launchInputEmbedding(&rid_t, &rin, &E);
+        LLaMAAttentionDynParams rp;
+        rp.batch_size = bs;
+        rp.num_tokens = tokens;
+        rp.max_q_len = maxq;
+        rp.max_k_len = maxq;
+        rp.num_layers = L;
+        TensorMap rcin{{"decoder_input", &rin}, {"history_length", &rhist_t}, {"input_length", &rq_t},
+                       {"context_length", &rk_t}, {"layer_id", &layer_t}};
+        TensorMap rcout{{"decoder_output", &rout}, {"all_k_cache", &rkcache}, {"all_v_cache", &rvcache}};
+        ctx.forward(rcin, lw, rcout, rp);
+        std::printf("{\"ragged_lens\": [%d, %d, %d], \"ragged_logits\": [", lens[0], lens[1], lens[2]);
+        int row = 0;
+        for (int b = 0; b < bs; ++b) {
+            row += lens[b];
+            TensorWrapper<float> lastb(GPU, FP32, {1, H}, ry.p + (size_t)(row - 1) * H);
+            launchRMSNorm(&lastb, &un, FN, 1e-5f, true);
+            launchLinearGemm(&lastb, LM, &probs, nullptr, false, true);
+            const std::vector<float> lg = logits.get();
+            std::printf("%s[", b ? ", " : "");
+            for (int i = 0; i < V; ++i) std::printf("%s%.7g", i ? "," : "", lg[i]);
+            std::printf("]");
+        }
+        std::printf("]}\n");
+    }
     for (auto* w : lw) delete w;
 }
 
