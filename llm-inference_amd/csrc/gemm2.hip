@@ -216,7 +216,9 @@ __global__ __launch_bounds__(kThreads) void gemm2_kernel(Gemm2Args a) {
 // v = x * rsqrt(mean(x^2) + eps) * gamma (the reference's order, modeling_llama.py:
 // 112-117); hi = fp16(v), lo = fp16(v - hi). The row stays in registers (NPT float4s
 // per thread, k <= NPT * 1024): x and the slab slices are read once, x written once.
-template <int NPT>
+// KS > 0: the slice count is a constant and every slice's loads are issued before the
+// first add (one memory round trip instead of one per slice); KS = 0: runtime ksplit.
+template <int NPT, int KS>
 __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx, int k, const void* gamma,
                                                              int g_dtype, float eps, _Float16* hi, _Float16* lo,
                                                              int ldh, const float* slab, int ksplit, int m) {
@@ -229,7 +231,24 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
         const int j = threadIdx.x + i * kThreads;
         v[i] = j < k4 ? reinterpret_cast<const float4*>(xr)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (slab) {  // split-K combine: x += slice 0 + slice 1 + ... (fixed order), written back
+    if (KS > 0 && slab) {  // split-K combine: x += slice 0 + slice 1 + ... (fixed order)
+        float4 p[KS > 0 ? KS : 1][NPT];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const float4* sl = reinterpret_cast<const float4*>(slab + ((size_t)s * m + blockIdx.x) * ldx);
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                const int j = threadIdx.x + i * kThreads;
+                p[s][i] = j < k4 ? sl[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                v[i].x += p[s][i].x; v[i].y += p[s][i].y; v[i].z += p[s][i].z; v[i].w += p[s][i].w;
+            }
+    } else if (slab) {
         for (int s = 0; s < ksplit; ++s) {
             const float4* sl = reinterpret_cast<const float4*>(slab + ((size_t)s * m + blockIdx.x) * ldx);
 #pragma unroll
@@ -241,6 +260,8 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
                 }
             }
         }
+    }
+    if (slab) {  // x written back
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
             const int j = threadIdx.x + i * kThreads;
@@ -358,15 +379,27 @@ int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_
     LLMI_REQUIRE(!slab || (ksplit >= 1 && ldx == k), "rows_split: slab rows must be dense (ldx == k)");
     LLMI_REQUIRE(k <= 8 * 4 * kThreads, "rows_split: rows longer than 8192 are not supported");
     const int npt = (k / 4 + kThreads - 1) / kThreads;
-#define RS_LAUNCH(N) \
-    hipLaunchKernelGGL(rows_split_kernel<N>, dim3(m), dim3(kThreads), 0, s, x, ldx, k, gamma, g_dtype, eps, hi, lo, ldh, \
-                       slab, ksplit, m)
+    // slice counts the prefill uses get the all-loads-first instance (o_proj 2, down 8)
+    const int ks = !slab ? 0 : (ksplit == 2 || (ksplit == 8 && npt <= 5)) ? ksplit : 0;
+#define RS_LAUNCH(N, S) \
+    hipLaunchKernelGGL((rows_split_kernel<N, S>), dim3(m), dim3(kThreads), 0, s, x, ldx, k, gamma, g_dtype, eps, hi, lo, \
+                       ldh, slab, ksplit, m)
+#define RS_KS(N) \
+    do {                                  \
+        if (ks == 2)                      \
+            RS_LAUNCH(N, 2);              \
+        else if (ks == 8 && (N) <= 5)     \
+            RS_LAUNCH(N, ((N) <= 5 ? 8 : 0)); \
+        else                              \
+            RS_LAUNCH(N, 0);              \
+    } while (0)
     if (npt <= 4)
-        RS_LAUNCH(4);
+        RS_KS(4);
     else if (npt <= 5)
-        RS_LAUNCH(5);
+        RS_KS(5);
     else
-        RS_LAUNCH(8);
+        RS_KS(8);
+#undef RS_KS
 #undef RS_LAUNCH
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
