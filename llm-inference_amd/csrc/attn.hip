@@ -34,11 +34,13 @@ namespace {
 
 using namespace attn_detail;
 
-template <typename KT>
-__global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a) {
+// ns: the workspace's split stride (max_seq / 64); the grid holds ns splits, or only
+// the a.nact active ones (HOST_SIZED)
+template <typename KT, bool HOST_SIZED>
+__global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a, int ns) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     WgStamp ts(a.stamps);
-    attn_body<KT, PlainIO>(a, blockIdx.x, blockIdx.y, gridDim.y, smem, NoSync{});
+    attn_body<KT, PlainIO, NoSync, HOST_SIZED>(a, blockIdx.x, blockIdx.y, ns, smem, NoSync{});
 }
 
 // Log-sum-exp merge of the split-KV partials of each head (one workgroup per
@@ -133,16 +135,27 @@ int attn_decode_launch(const AttnArgs& a, hipStream_t s) {
     LLMI_REQUIRE(a.qkv && a.k_cache && a.v_cache && a.workspace, "attn: null pointer");
     LLMI_REQUIRE(!a.direct_out || a.out, "attn: null output");
     LLMI_REQUIRE(!a.xacc || a.resid || a.resid_fixed, "attn: xacc seeding needs resid");
-    const dim3 grid(a.heads, (a.max_seq + CH - 1) / CH);  // ns = gridDim.y
-    if (a.cache_dtype == LLMI_F16)
-        hipLaunchKernelGGL(attn_decode_kernel<__half>, grid, dim3(kThreads), kAttnLds, s, a);
-    else if (a.cache_dtype == LLMI_F32)
-        hipLaunchKernelGGL(attn_decode_kernel<float>, grid, dim3(kThreads), kAttnLds, s, a);
-    else
+    const int ns = (a.max_seq + CH - 1) / CH;
+    LLMI_REQUIRE(a.nact >= 0 && a.nact <= ns, "attn: nact out of range");
+    LLMI_REQUIRE(a.pos_dev || a.nact == 0 || a.nact == a.pos_host / CH + 1, "attn: nact != ceil((pos + 1) / 64)");
+    const bool hs = a.nact > 0;
+    const dim3 grid(a.heads, hs ? a.nact : ns);
+    if (a.cache_dtype == LLMI_F16) {
+        if (hs)
+            hipLaunchKernelGGL((attn_decode_kernel<__half, true>), grid, dim3(kThreads), kAttnLds, s, a, ns);
+        else
+            hipLaunchKernelGGL((attn_decode_kernel<__half, false>), grid, dim3(kThreads), kAttnLds, s, a, ns);
+    } else if (a.cache_dtype == LLMI_F32) {
+        if (hs)
+            hipLaunchKernelGGL((attn_decode_kernel<float, true>), grid, dim3(kThreads), kAttnLds, s, a, ns);
+        else
+            hipLaunchKernelGGL((attn_decode_kernel<float, false>), grid, dim3(kThreads), kAttnLds, s, a, ns);
+    } else {
         LLMI_REQUIRE(false, "attn: cache dtype must be f16 or f32");
+    }
     LLMI_HIP(hipGetLastError());
     if (a.direct_out) {
-        hipLaunchKernelGGL(attn_merge_kernel, dim3(a.heads), dim3(kThreads), 0, s, a, (int)grid.y);
+        hipLaunchKernelGGL(attn_merge_kernel, dim3(a.heads), dim3(kThreads), 0, s, a, ns);
         LLMI_HIP(hipGetLastError());
     }
     return LLMI_OK;
@@ -153,6 +166,7 @@ int attn_oproj_launch(const OprojArgs& a, hipStream_t s) {
     LLMI_REQUIRE(a.w && a.workspace && a.xacc && a.heads > 0 && a.n_rows > 0, "attn_oproj: bad arguments");
     LLMI_REQUIRE(a.ldw >= a.heads * D, "attn_oproj: ldw < heads * head_dim");
     LLMI_REQUIRE(a.max_seq > 0 && (a.max_seq + CH - 1) / CH <= kMaxSplits, "attn_oproj: max_seq out of range");
+    LLMI_REQUIRE(a.nact >= 0 && a.nact <= (a.max_seq + CH - 1) / CH, "attn_oproj: nact out of range");
     switch (a.w_dtype) {
         case LLMI_F16: return oproj_launch_w<__half>(a, s);
         case LLMI_F32: return oproj_launch_w<float>(a, s);

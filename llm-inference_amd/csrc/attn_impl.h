@@ -154,7 +154,11 @@ constexpr size_t kAttnLds = (3 * D + CH + (kThreads / LPR) * D + 4) * sizeof(flo
 // One (head h, split) workgroup of the split-KV decode attention. ns = number of
 // splits (workspace stride). In the dataflow kernel (SYNC::kFlow) the K/V loads are
 // issued, then the wait for the q/k/v projection, then the sc1 reads of q, k, v.
-template <typename KT, typename IO, typename SYNC>
+// HOST_SIZED (a.nact > 0): the grid holds only the active splits, so the K/V row
+// loads are issued from the kernel arguments alone, before the device position (a
+// scalar load from memory another kernel just wrote) has arrived; rows past the
+// position are loaded (valid cache memory below max_seq) and ignored.
+template <typename KT, typename IO, typename SYNC, bool HOST_SIZED = false>
 __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, int ns, float* smem,
                                           const SYNC& sync) {
     float* q_s = smem;
@@ -164,32 +168,44 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     float (*o_red)[D] = reinterpret_cast<float (*)[D]>(p_s + CH);  // [groups][D]
     float* ml_s = p_s + CH + (kThreads / LPR) * D;
 
-    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
-    if (pos < 0 || pos >= a.max_seq) return;  // host validates; guard against a stale state
-    const int ctx = pos + 1;
-    const int start = split * CH;
-    if (start >= ctx) return;
-    const int end = min(start + CH, ctx);
-    const int nact = (ctx + CH - 1) / CH;
     const int group = a.heads / a.kv_heads;
     const int kvh = h / group;
     const int tid = threadIdx.x;
-    const bool owns_pos = (end == ctx);
     const int grp = tid / LPR, l16 = tid % LPR;  // 16 groups x 16 lanes, 8 dims per lane
+    const int start = split * CH;
+    KT* kc = reinterpret_cast<KT*>(a.k_cache) + (size_t)kvh * a.max_seq * D;
+    KT* vc = reinterpret_cast<KT*>(a.v_cache) + (size_t)kvh * a.max_seq * D;
+    Raw<KT> kr[NPG], vr[NPG];
+    if constexpr (HOST_SIZED) {
+#pragma unroll
+        for (int t = 0; t < NPG; ++t) {
+            const int j = start + grp + t * (kThreads / LPR);
+            const int jj = j < a.max_seq ? j : start;
+            kr[t] = ld_raw(kc + (size_t)jj * D + l16 * 8);
+            vr[t] = ld_raw(vc + (size_t)jj * D + l16 * 8);
+        }
+    }
+
+    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
+    if (pos < 0 || pos >= a.max_seq) return;  // host validates; guard against a stale state
+    const int ctx = pos + 1;
+    if (start >= ctx) return;
+    const int end = min(start + CH, ctx);
+    const int nact = (ctx + CH - 1) / CH;
+    const bool owns_pos = (end == ctx);
 
     // ---- issue every K and V row load of this block first: they do not depend on
     // q, so their HBM latency overlaps the q/RoPE prologue (NPG rows per lane each)
-    KT* kc = reinterpret_cast<KT*>(a.k_cache) + (size_t)kvh * a.max_seq * D;
-    KT* vc = reinterpret_cast<KT*>(a.v_cache) + (size_t)kvh * a.max_seq * D;
     // branch-free: rows past `end` or at `pos` load a valid row (start) and are ignored
     // later -- a predicated load would serialise the stream on vmcnt(0) waits
-    Raw<KT> kr[NPG], vr[NPG];
+    if constexpr (!HOST_SIZED) {
 #pragma unroll
-    for (int t = 0; t < NPG; ++t) {
-        const int j = start + grp + t * (kThreads / LPR);
-        const int jj = (j < end && j != pos) ? j : start;
-        kr[t] = ld_raw(kc + (size_t)jj * D + l16 * 8);
-        vr[t] = ld_raw(vc + (size_t)jj * D + l16 * 8);
+        for (int t = 0; t < NPG; ++t) {
+            const int j = start + grp + t * (kThreads / LPR);
+            const int jj = (j < end && j != pos) ? j : start;
+            kr[t] = ld_raw(kc + (size_t)jj * D + l16 * 8);
+            vr[t] = ld_raw(vc + (size_t)jj * D + l16 * 8);
+        }
     }
 
     sync.wait();  // dataflow: q/k/v of this token are published by the projection phase
@@ -373,6 +389,9 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
     const float* mlh = ws.ml + (size_t)h * ns * 2;
     const float* oh = ws.o + (size_t)h * ns * D + d;
     float ov[kMergeChunk];
+    // splits to load: the host-known active count, else every split (the position
+    // decides which are used)
+    const int nl = a.nact > 0 ? min(a.nact, ns) : ns;
     W8<WT> wr_own[NPL];
     W8<WT> (&wr)[NPL] = PRE ? *pre : wr_own;
     auto load_w = [&]() {
@@ -399,14 +418,14 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
 #pragma unroll
     for (int i = 0; i < kMergeChunk; ++i) {
         const int sp = half + 2 * i;
-        ov[i] = IO::ld(oh + (size_t)(sp < ns ? sp : 0) * D);
+        ov[i] = IO::ld(oh + (size_t)(sp < nl ? sp : 0) * D);
     }
     constexpr int kMlPer = kMaxSplits / kThreads;
     float mr[kMlPer], lr[kMlPer];
 #pragma unroll
     for (int i = 0; i < kMlPer; ++i) {
-        if (i * kThreads < ns) {  // uniform branch: no per-lane predication of the loads
-            const int sp = min(tid + i * kThreads, ns - 1);
+        if (i * kThreads < nl) {  // uniform branch: no per-lane predication of the loads
+            const int sp = min(tid + i * kThreads, nl - 1);
             mr[i] = IO::ld(mlh + 2 * sp);
             lr[i] = IO::ld(mlh + 2 * sp + 1);
         }
@@ -415,13 +434,16 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
 #pragma unroll
     for (int i = 0; i < kMlPer; ++i) {
         const int sp = tid + i * kThreads;
-        if (i * kThreads < ns && sp < ns) {
+        if (i * kThreads < nl && sp < nl) {
             m_s[sp] = mr[i];
             l_s[sp] = lr[i];
         }
     }
-    if (pos < 0 || pos >= a.max_seq) return;
-    const int nact = (pos + 1 + CH - 1) / CH;
+    int nact = nl;
+    if (a.nact <= 0) {
+        if (pos < 0 || pos >= a.max_seq) return;
+        nact = (pos + 1 + CH - 1) / CH;
+    }
     __syncthreads();
     // log-sum-exp weights by wave 0 (one expf per split), into LDS
     if (tid < kWave) {

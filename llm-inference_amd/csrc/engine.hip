@@ -49,6 +49,45 @@ namespace {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace
 
+// The token graphs, one per active split count nact = pos / 64 + 1: the attention
+// and o_proj grids are sized on the host (AttnArgs::nact), so one captured step is
+// valid for 64 consecutive positions. Built lazily, before a decode run's launches.
+struct StepGraphs {
+    std::vector<hipGraph_t> g;
+    std::vector<hipGraphExec_t> x;
+    void clear() {
+        for (auto e : x)
+            if (e) (void)hipGraphExecDestroy(e);
+        for (auto h : g)
+            if (h) (void)hipGraphDestroy(h);
+        x.clear();
+        g.clear();
+    }
+    ~StepGraphs() { clear(); }
+    bool empty() const { return x.empty(); }
+    // capture record() (which records one step for nact) on s unless cached
+    template <typename F>
+    int build(int nact, hipStream_t s, F&& record) {
+        if ((int)x.size() <= nact) {
+            x.resize(nact + 1, nullptr);
+            g.resize(nact + 1, nullptr);
+        }
+        if (x[nact]) return LLMI_OK;
+        LLMI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        int rc = record();
+        hipGraph_t h = nullptr;
+        hipError_t e = hipStreamEndCapture(s, &h);
+        if (rc != LLMI_OK) {
+            if (h) (void)hipGraphDestroy(h);
+            return rc;
+        }
+        LLMI_HIP(e);
+        g[nact] = h;
+        LLMI_HIP(hipGraphInstantiate(&x[nact], h, nullptr, nullptr, 0));
+        return LLMI_OK;
+    }
+};
+
 struct Engine {
     llmi_config c{};
     int device = 0;
@@ -90,8 +129,8 @@ struct Engine {
     DecodeState* st = nullptr;
     int32_t *prompt = nullptr, *tokens = nullptr;
 
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
+    StepGraphs graphs;
+    int rec_nact = 0;  // active split count the next recorded step's attention is sized for
     ncclComm_t comm = nullptr;
     // prefill scratch (allocated on first use): rows of one prefill chunk
     char* pf = nullptr;
@@ -117,8 +156,7 @@ struct Engine {
     ~Engine() {  // teardown errors are not actionable; ignore them explicitly
         if (samp_ids) (void)hipFree(samp_ids);
         if (samp_vals) (void)hipFree(samp_vals);
-        if (exec) (void)hipGraphExecDestroy(exec);
-        if (graph) (void)hipGraphDestroy(graph);
+        graphs.clear();
         if (comm) (void)ncclCommDestroy(comm);
         if (wblob) (void)hipFree(wblob);
         if (kcache) (void)hipFree(kcache);
@@ -518,6 +556,7 @@ struct Engine {
         a.resid_scale = (c.tp_rank == 0) ? 1.f : 0.f;  // rank 0 carries the residual into the all-reduce
         a.hidden = c.hidden;
         a.out = attn_out; a.workspace = attn_ws;
+        a.nact = rec_nact;
         return a;
     }
     OprojArgs o_args(int l) const {
@@ -530,6 +569,7 @@ struct Engine {
         a.heads = hl; a.head_dim = c.head_dim; a.max_seq = c.max_seq;
         a.pos_dev = &st->cur_pos;
         a.workspace = attn_ws; a.xacc = xacc;
+        a.nact = rec_nact;
         return a;
     }
     GemvArgs gu_args(int l) const {
@@ -589,14 +629,9 @@ struct Engine {
             LLMI_HIP(hipMalloc(&samp_ids, 16 * sizeof(int32_t)));
             LLMI_HIP(hipMalloc(&samp_vals, 16 * sizeof(float)));
         }
-        if (exec) {  // the captured step changes: re-capture on the next graph decode
+        if (!graphs.empty()) {  // the captured step changes: re-capture on the next graph decode
             LLMI_HIP(hipStreamSynchronize(stream));  // a replay may still be in flight
-            LLMI_HIP(hipGraphExecDestroy(exec));
-            exec = nullptr;
-        }
-        if (graph) {
-            LLMI_HIP(hipGraphDestroy(graph));
-            graph = nullptr;
+            graphs.clear();
         }
         sample_k = k;
         sample_seed = sd;
@@ -627,20 +662,10 @@ struct Engine {
         return LLMI_OK;
     }
 
-    int build_graph() {
-        if (exec) return LLMI_OK;
-        LLMI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-        int rc = record_step();
-        hipGraph_t g = nullptr;
-        hipError_t e = hipStreamEndCapture(stream, &g);
-        if (rc != LLMI_OK) {
-            if (g) (void)hipGraphDestroy(g);
-            return rc;
-        }
-        LLMI_HIP(e);
-        graph = g;
-        LLMI_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-        return LLMI_OK;
+    static int nact_of(int pos) { return pos / kAttnChunk + 1; }
+    int build_graph(int nact) {
+        rec_nact = nact;
+        return graphs.build(nact, stream, [&]() { return record_step(); });
     }
 
     // ------------------------------------------------------------- driving
@@ -665,12 +690,16 @@ struct Engine {
     int decode(int n, int use_graph) {
         LLMI_REQUIRE(prompt_len > 0, "decode: set_prompt first");
         LLMI_REQUIRE(n >= 0 && host_next_pos + n <= c.max_seq, "decode: would run past max_seq");
-        if (use_graph) LLMI_TRY(build_graph());
+        if (use_graph && n > 0)  // every graph this run replays, captured before the first launch
+            for (int k = nact_of(host_next_pos); k <= nact_of(host_next_pos + n - 1); ++k) LLMI_TRY(build_graph(k));
         for (int i = 0; i < n; ++i) {
-            if (use_graph)
-                LLMI_HIP(hipGraphLaunch(exec, stream));
-            else
+            const int k = nact_of(host_next_pos + i);
+            if (use_graph) {
+                LLMI_HIP(hipGraphLaunch(graphs.x[k], stream));
+            } else {
+                rec_nact = k;
                 LLMI_TRY(record_step());
+            }
         }
         host_next_pos += n;
         return LLMI_OK;
@@ -886,12 +915,10 @@ struct Group {
     std::vector<std::unique_ptr<Engine>> r;
     hipStream_t stream = nullptr;
     void** ptrs = nullptr;  // device [4][W]: xacc, res[0], res[1], partials of every rank
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
+    StepGraphs graphs;
 
     ~Group() {
-        if (exec) (void)hipGraphExecDestroy(exec);
-        if (graph) (void)hipGraphDestroy(graph);
+        graphs.clear();
         r.clear();
         if (ptrs) (void)hipFree(ptrs);
         if (stream) (void)hipStreamDestroy(stream);
@@ -920,8 +947,9 @@ struct Group {
         return LLMI_OK;
     }
 
-    int record_step() {
+    int record_step(int nact) {
         const int W = (int)r.size(), H = r[0]->c.hidden;
+        for (auto& e : r) e->rec_nact = nact;
         for (auto& e : r) LLMI_TRY(e->rec_start());
         for (int l = 0; l < r[0]->c.layers; ++l) {
             for (auto& e : r) LLMI_TRY(e->rec_attn(l));
@@ -938,24 +966,15 @@ struct Group {
         Engine& e0 = *r[0];
         LLMI_REQUIRE(e0.prompt_len > 0, "group decode: set_prompt first");
         LLMI_REQUIRE(n >= 0 && e0.host_next_pos + n <= e0.c.max_seq, "group decode: would run past max_seq");
-        if (use_graph && !exec) {
-            LLMI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-            int rc = record_step();
-            hipGraph_t g = nullptr;
-            hipError_t err = hipStreamEndCapture(stream, &g);
-            if (rc != LLMI_OK) {
-                if (g) (void)hipGraphDestroy(g);
-                return rc;
-            }
-            LLMI_HIP(err);
-            graph = g;
-            LLMI_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-        }
+        if (use_graph && n > 0)
+            for (int k = Engine::nact_of(e0.host_next_pos); k <= Engine::nact_of(e0.host_next_pos + n - 1); ++k)
+                LLMI_TRY(graphs.build(k, stream, [&]() { return record_step(k); }));
         for (int i = 0; i < n; ++i) {
+            const int k = Engine::nact_of(e0.host_next_pos + i);
             if (use_graph)
-                LLMI_HIP(hipGraphLaunch(exec, stream));
+                LLMI_HIP(hipGraphLaunch(graphs.x[k], stream));
             else
-                LLMI_TRY(record_step());
+                LLMI_TRY(record_step(k));
         }
         for (auto& e : r) e->host_next_pos += n;
         return LLMI_OK;
@@ -1183,6 +1202,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     Engine& g = e->e;
     LLMI_HIP(hipSetDevice(g.device));
     LLMI_REQUIRE(g.prompt_len > 0 && g.host_next_pos > 0, "time_kernel: decode at least one step first");
+    g.rec_nact = Engine::nact_of(g.host_next_pos - 1);  // attention sized for the current position
     const size_t H = g.c.hidden;
     uint64_t b = 0;
     // launch i uses layer i % layers: every launch streams weights (and KV) the

@@ -163,6 +163,11 @@ struct AttnArgs {
     const long long* resid_fixed = nullptr;
     float resid_scale = 1.f;
     int hidden = 0;
+    // > 0: the caller knows the position's split count, ceil((pos + 1) / 64) (the engine
+    // tracks the position on the host): the grid is exactly the active splits and every
+    // K/V load is issued before the device position arrives; 0: grid = max_seq / 64,
+    // inactive splits exit after reading the position
+    int nact = 0;
 };
 
 // Merge of the split partials fused into the o_proj, split by head: workgroup
@@ -182,6 +187,7 @@ struct OprojArgs {
     int pos_host = 0;
     const void* workspace = nullptr;  // attention partials
     long long* xacc = nullptr;
+    int nact = 0;  // > 0: active split count known on the host (no position read); see AttnArgs
 };
 int attn_oproj_launch(const OprojArgs& a, hipStream_t s);
 // fixed-point residual accumulator: value = int64 * 2^-32
