@@ -36,6 +36,23 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(REPO, "include", "*.h"))
 
 
+def _includes(path, seen=None):
+    """path plus every csrc/include header it pulls in through #include "..." (transitively)."""
+    import re
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path, errors="replace") as f:
+        for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            for d in (os.path.dirname(path), CSRC, os.path.join(REPO, "include")):
+                q = os.path.normpath(os.path.join(d, m.group(1)))
+                if os.path.exists(q):
+                    _includes(q, seen)
+                    break
+    return seen
+
+
 def _stale(target, deps):
     if not os.path.exists(target):
         return True
@@ -61,7 +78,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> str:
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s)[:-4] + ".o")
         objs.append(o)
-        if force or _stale(o, [s, *hdrs]):
+        if force or _stale(o, sorted(_includes(s))):
             todo.append((s, o))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

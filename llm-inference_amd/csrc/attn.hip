@@ -138,6 +138,7 @@ int attn_decode_launch(const AttnArgs& a, hipStream_t s) {
     const int ns = (a.max_seq + CH - 1) / CH;
     LLMI_REQUIRE(a.nact >= 0 && a.nact <= ns, "attn: nact out of range");
     LLMI_REQUIRE(a.pos_dev || a.nact == 0 || a.nact == a.pos_host / CH + 1, "attn: nact != ceil((pos + 1) / 64)");
+    LLMI_REQUIRE(a.nact == 0 || a.pos_dev, "attn: nact > 0 needs the device position");
     const bool hs = a.nact > 0;
     const dim3 grid(a.heads, hs ? a.nact : ns);
     if (a.cache_dtype == LLMI_F16) {

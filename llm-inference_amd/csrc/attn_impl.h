@@ -175,8 +175,26 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     const int start = split * CH;
     KT* kc = reinterpret_cast<KT*>(a.k_cache) + (size_t)kvh * a.max_seq * D;
     KT* vc = reinterpret_cast<KT*>(a.v_cache) + (size_t)kvh * a.max_seq * D;
+    const float* qrow = a.qkv + (size_t)h * D;
+    const float* krow = a.qkv + (size_t)(a.heads + kvh) * D;
+    const float* vrow = a.qkv + (size_t)(a.heads + a.kv_heads + kvh) * D;
+    const int seed_per = (a.hidden + a.heads - 1) / a.heads;  // residual slice split 0 seeds
     Raw<KT> kr[NPG], vr[NPG];
+    // HOST_SIZED prologue: every load that does not need the position goes out before
+    // anything waits (vmcnt retires in issue order, so the position is issued first --
+    // the RoPE table read depends on it): K/V rows, the q row, the current k/v rows,
+    // the residual slice split 0 seeds. Each is one round trip in parallel instead of
+    // the position -> K/V -> q -> table chain (4 serial round trips).
+    float pq0 = 0.f, pq1 = 0.f, pk0 = 0.f, pk1 = 0.f, pv = 0.f;
+    long long psd = 0;
+    int pos;
     if constexpr (HOST_SIZED) {
+        // the launcher requires a device position here. The load goes through a per-lane
+        // (opaque zero) index so the compiler keeps it in a VGPR: as a uniform value it was
+        // moved to an SGPR right after the load, with a vmcnt wait in front of the K/V issue
+        int z = 0;
+        asm volatile("" : "+v"(z));
+        pos = a.pos_dev[z];
 #pragma unroll
         for (int t = 0; t < NPG; ++t) {
             const int j = start + grp + t * (kThreads / LPR);
@@ -184,9 +202,20 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
             kr[t] = ld_raw(kc + (size_t)jj * D + l16 * 8);
             vr[t] = ld_raw(vc + (size_t)jj * D + l16 * 8);
         }
+        const int i = tid & (D / 2 - 1);
+        pq0 = IO::ld(qrow + i);
+        pq1 = IO::ld(qrow + i + D / 2);
+        // the current k and v (used by the split owning the position; loaded by every
+        // split: a branch here made the compiler convert them, and so wait, early)
+        pk0 = IO::ld(krow + i);
+        pk1 = IO::ld(krow + i + D / 2);
+        pv = IO::ld(vrow + (tid & (D - 1)));
+        if (a.xacc != nullptr && split == 0 && a.resid_fixed != nullptr)
+            psd = a.resid_fixed[min(h * seed_per + tid, a.hidden - 1)];
+    } else {
+        pos = a.pos_dev ? *a.pos_dev : a.pos_host;
     }
 
-    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
     if (pos < 0 || pos >= a.max_seq) return;  // host validates; guard against a stale state
     const int ctx = pos + 1;
     if (start >= ctx) return;
@@ -211,9 +240,6 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     sync.wait();  // dataflow: q/k/v of this token are published by the projection phase
 
     // ---- q (and the current k, v when this block owns position `pos`)
-    const float* qrow = a.qkv + (size_t)h * D;
-    const float* krow = a.qkv + (size_t)(a.heads + kvh) * D;
-    const float* vrow = a.qkv + (size_t)(a.heads + a.kv_heads + kvh) * D;
     const float qscale = 1.0f / sqrtf((float)D);
     if (tid < D / 2) {
         const int i = tid;
@@ -226,16 +252,16 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
             rope_cs(pos, i, D, a.rope_base, &c, &s);
         }
         // rotate_half pairing (i, i + d/2): modeling_llama.py:204-235
-        const float q0 = IO::ld(qrow + i), q1 = IO::ld(qrow + i + D / 2);
+        const float q0 = HOST_SIZED ? pq0 : IO::ld(qrow + i), q1 = HOST_SIZED ? pq1 : IO::ld(qrow + i + D / 2);
         q_s[i] = (q0 * c - q1 * s) * qscale;
         q_s[i + D / 2] = (q1 * c + q0 * s) * qscale;
         if (owns_pos) {
-            const float k0 = IO::ld(krow + i), k1 = IO::ld(krow + i + D / 2);
+            const float k0 = HOST_SIZED ? pk0 : IO::ld(krow + i), k1 = HOST_SIZED ? pk1 : IO::ld(krow + i + D / 2);
             kcur_s[i] = cache_round<KT>(k0 * c - k1 * s);
             kcur_s[i + D / 2] = cache_round<KT>(k1 * c + k0 * s);
         }
     } else if (owns_pos && tid >= D && tid < 2 * D) {
-        vcur_s[tid - D] = cache_round<KT>(IO::ld(vrow + tid - D));
+        vcur_s[tid - D] = cache_round<KT>(HOST_SIZED ? pv : IO::ld(vrow + tid - D));
     }
     __syncthreads();
 
@@ -325,9 +351,14 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     // the next kernel (attn_oproj) with its 128-element slice: fixed(resid) on the
     // rank that carries the residual (TP rank 0), zero elsewhere
     if (a.xacc != nullptr && split == 0) {
-        const int per = (a.hidden + a.heads - 1) / a.heads;
-        for (int i = h * per + tid; i < min((h + 1) * per, a.hidden); i += kThreads)
-            IO::st_ll(a.xacc + i, a.resid_scale == 0.f ? 0ll : a.resid_fixed ? a.resid_fixed[i] : to_fixed(a.resid[i]));
+        const int per = seed_per;
+        for (int i = h * per + tid; i < min((h + 1) * per, a.hidden); i += kThreads) {
+            const bool pre = HOST_SIZED && a.resid_fixed && i == h * per + (int)tid;  // prefetched in the prologue
+            IO::st_ll(a.xacc + i, a.resid_scale == 0.f ? 0ll
+                                  : pre            ? psd
+                                  : a.resid_fixed  ? a.resid_fixed[i]
+                                                   : to_fixed(a.resid[i]));
+        }
     }
 }
 
@@ -378,7 +409,6 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
     float* o_s = l_s + kMaxSplits + 4;
     float (*o_red)[D] = reinterpret_cast<float (*)[D]>(o_s + D);
     float* y_s = o_s + 3 * D;
-    const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;  // scalar load, issued first
     const int tid = threadIdx.x;
     const int grp = tid / LPR, l16 = tid % LPR;
     const int row0 = chunk * 16 * NPL;
@@ -440,7 +470,8 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
         }
     }
     int nact = nl;
-    if (a.nact <= 0) {
+    if (a.nact <= 0) {  // position-derived split count (its load waits here, after the W_o issue)
+        const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
         if (pos < 0 || pos >= a.max_seq) return;
         nact = (pos + 1 + CH - 1) / CH;
     }

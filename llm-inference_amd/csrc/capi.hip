@@ -105,7 +105,6 @@ int llmi_attn_decode(const float* qkv, void* k_cache, void* v_cache, int cache_d
     a.rope_base = rope_base;
     a.out = out;
     a.workspace = workspace;
-    if (pos >= 0 && pos < max_seq) a.nact = pos / kAttnChunk + 1;  // host position: grid = active splits
     return attn_decode_launch(a, STREAM(stream));
 }
 
