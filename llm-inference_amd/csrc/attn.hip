@@ -101,6 +101,9 @@ __global__ __launch_bounds__(kThreads) void attn_oproj_kernel(OprojArgs a, int n
 
 int oproj_npl(const OprojArgs& a) {
     const long target = (long)a.heads * a.n_rows / (1024 * 16);  // ~1024 workgroups
+#ifdef LLMI_OPROJ_NPL
+    if (target >= 8) return LLMI_OPROJ_NPL;
+#endif
     return target >= 8 ? 8 : target >= 4 ? 4 : target >= 2 ? 2 : 1;
 }
 
@@ -111,6 +114,9 @@ int oproj_launch_w(const OprojArgs& a, hipStream_t s) {
     const int npl = oproj_npl(a);
     const dim3 grid(a.heads, (a.n_rows + 16 * npl - 1) / (16 * npl));
     switch (npl) {
+#if LLMI_OPROJ_NPL == 16
+        case 16: hipLaunchKernelGGL((attn_oproj_kernel<WT, 16>), grid, dim3(kThreads), oproj_lds<16>(), s, a, ns); break;
+#endif
         case 8: hipLaunchKernelGGL((attn_oproj_kernel<WT, 8>), grid, dim3(kThreads), oproj_lds<8>(), s, a, ns); break;
         case 4: hipLaunchKernelGGL((attn_oproj_kernel<WT, 4>), grid, dim3(kThreads), oproj_lds<4>(), s, a, ns); break;
         case 2: hipLaunchKernelGGL((attn_oproj_kernel<WT, 2>), grid, dim3(kThreads), oproj_lds<2>(), s, a, ns); break;

@@ -26,7 +26,7 @@ def role(name):
         return "lm_head"
     if "gemv_kernel<__half, 2, 4," in name:
         return "down"
-    if "attn_decode_kernel<__half>" in name:
+    if "attn_decode_kernel<__half>" in name or "attn_decode_kernel<__half, " in name:
         return "attn"
     if "attn_oproj_kernel<__half" in name:
         return "o"
