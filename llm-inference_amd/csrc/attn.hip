@@ -40,7 +40,7 @@ template <typename KT, bool HOST_SIZED>
 __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a, int ns) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     WgStamp ts(a.stamps);
-    attn_body<KT, PlainIO, NoSync, HOST_SIZED>(a, blockIdx.x, blockIdx.y, ns, smem, NoSync{});
+    attn_body<KT, PlainIO, HOST_SIZED>(a, blockIdx.x, blockIdx.y, ns, smem);
 }
 
 // Log-sum-exp merge of the split-KV partials of each head (one workgroup per
@@ -96,7 +96,7 @@ template <typename WT, int NPL>
 __global__ __launch_bounds__(kThreads) void attn_oproj_kernel(OprojArgs a, int ns) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     WgStamp ts(a.stamps);
-    oproj_body<WT, NPL, PlainIO>(a, blockIdx.x, blockIdx.y, ns, smem, NoSync{});
+    oproj_body<WT, NPL, PlainIO>(a, blockIdx.x, blockIdx.y, ns, smem);
 }
 
 int oproj_npl(const OprojArgs& a) {

@@ -1,8 +1,8 @@
-// Decode attention bodies shared by the standalone kernels (attn.hip) and the
-// dataflow layer kernel (layer.hip): split-KV attention with the KV-cache write,
-// and the fused log-sum-exp merge + o_proj. See attn.hip for the design notes.
+// Decode attention bodies of the kernels in attn.hip: split-KV attention with the
+// KV-cache write, and the fused log-sum-exp merge + o_proj. See attn.hip for the
+// design notes.
 #pragma once
-#include "handoff.h"
+#include "io.h"
 #include "kernels.h"
 
 namespace llmi {
@@ -152,15 +152,13 @@ __device__ __forceinline__ void unpack_w8(const W8<WT>& r, float* v) {
 constexpr size_t kAttnLds = (3 * D + CH + (kThreads / LPR) * D + 4) * sizeof(float);
 
 // One (head h, split) workgroup of the split-KV decode attention. ns = number of
-// splits (workspace stride). In the dataflow kernel (SYNC::kFlow) the K/V loads are
-// issued, then the wait for the q/k/v projection, then the sc1 reads of q, k, v.
+// splits (workspace stride).
 // HOST_SIZED (a.nact > 0): the grid holds only the active splits, so the K/V row
 // loads are issued from the kernel arguments alone, before the device position (a
 // scalar load from memory another kernel just wrote) has arrived; rows past the
 // position are loaded (valid cache memory below max_seq) and ignored.
-template <typename KT, typename IO, typename SYNC, bool HOST_SIZED = false>
-__device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, int ns, float* smem,
-                                          const SYNC& sync) {
+template <typename KT, typename IO, bool HOST_SIZED = false>
+__device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, int ns, float* smem) {
     float* q_s = smem;
     float* kcur_s = q_s + D;
     float* vcur_s = kcur_s + D;
@@ -236,8 +234,6 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
             vr[t] = ld_raw(vc + (size_t)jj * D + l16 * 8);
         }
     }
-
-    sync.wait();  // dataflow: q/k/v of this token are published by the projection phase
 
     // ---- q (and the current k, v when this block owns position `pos`)
     const float qscale = 1.0f / sqrtf((float)D);
@@ -398,11 +394,8 @@ __device__ __forceinline__ void oproj_load_w(const OprojArgs& a, int h, int chun
     }
 }
 
-// PRE: the W_o slice was issued by the caller (oproj_load_w into *pre) before
-// other work; SYNC::kFlow: wait for the partials' producers after the W_o issue.
-template <typename WT, int NPL, typename IO, typename SYNC, bool PRE = false>
-__device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk, int ns, float* smem,
-                                           const SYNC& sync, W8<WT> (*pre)[NPL] = nullptr) {
+template <typename WT, int NPL, typename IO>
+__device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk, int ns, float* smem) {
     float* m_s = smem;
     float* l_s = m_s + kMaxSplits;
     float& linv_s = l_s[kMaxSplits];
@@ -422,21 +415,13 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
     // splits to load: the host-known active count, else every split (the position
     // decides which are used)
     const int nl = a.nact > 0 ? min(a.nact, ns) : ns;
-    W8<WT> wr_own[NPL];
-    W8<WT> (&wr)[NPL] = PRE ? *pre : wr_own;
-    auto load_w = [&]() {
-        if constexpr (!PRE) oproj_load_w<WT, NPL>(a, h, chunk, wr_own);
-    };
+    W8<WT> wr[NPL];
+    auto load_w = [&]() { oproj_load_w<WT, NPL>(a, h, chunk, wr); };
     (void)w;
-    // issue order: standalone -- partials first (needed first), then the W_o slice,
-    // all into registers before anything waits (a load stored straight to LDS makes
-    // the compiler wait for it -- and for every load issued before it -- right
-    // there, which had serialised the partials' latency in front of the W_o stream);
-    // dataflow -- the W_o slice first (independent of the attention phase), wait, partials
-    if constexpr (SYNC::kFlow) {
-        load_w();
-        sync.wait();
-    }
+    // issue order: partials first (needed first), then the W_o slice, all into
+    // registers before anything waits (a load stored straight to LDS makes the compiler
+    // wait for it -- and for every load issued before it -- right there, which had
+    // serialised the partials' latency in front of the W_o stream)
 #if LLMI_OPROJ_NOMERGE  // diagnostic only (wrong output): no partial loads, no merge
     if (true) {
         load_w();
@@ -460,7 +445,7 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
             lr[i] = IO::ld(mlh + 2 * sp + 1);
         }
     }
-    if constexpr (!SYNC::kFlow) load_w();
+    load_w();
 #pragma unroll
     for (int i = 0; i < kMlPer; ++i) {
         const int sp = tid + i * kThreads;

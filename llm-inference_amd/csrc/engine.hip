@@ -897,7 +897,7 @@ struct Engine {
         DecodeState h;
         LLMI_HIP(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
         LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error) +
-                                       " (1: token id out of range, 2: position overflow, 4: dataflow wait timed out)");
+                                       " (1: token id out of range, 2: position overflow)");
         const int m = n < valid ? n : valid;
         if (m > 0) LLMI_HIP(hipMemcpy(out, tokens, (size_t)m * 4, hipMemcpyDeviceToHost));
         if (n_valid) *n_valid = valid;

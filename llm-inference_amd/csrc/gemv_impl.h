@@ -1,9 +1,6 @@
-// GEMV body shared by the standalone gemv_kernel (gemv.hip) and the dataflow
-// layer kernel (layer.hip). See gemv.hip for the design notes; IO selects plain
-// or write-through (sc1) access for the activation bytes another workgroup of
-// the same launch produces or consumes, SYNC the dataflow wait/publish.
+// GEMV body of gemv_kernel (gemv_launch.h; design notes in gemv.hip).
 #pragma once
-#include "handoff.h"
+#include "io.h"
 #include "kernels.h"
 
 namespace llmi {
@@ -89,11 +86,9 @@ __host__ __device__ inline size_t gemv_lds_bytes(int k) { return (size_t)k * 4 +
 // XPT: float4s of x each thread holds in registers during staging (k <= XPT*4*256);
 // 0 = generic strided staging (standalone only).
 // bid / nblk: this workgroup's index in the GEMV grid and the grid size.
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, typename IO,
-          typename SYNC>
-__device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, float4* xs, const SYNC& sync) {
-    // residual hand-over (seed_dst <- seed_src slice); in the dataflow kernel seed_src
-    // is the previous phase's output, so it runs after the wait (below)
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, typename IO>
+__device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, float4* xs) {
+    // residual hand-over (seed_dst <- seed_src slice)
     auto seed = [&, bid0 = bid, nblk0 = nblk]() {
         if (a.seed_dst == nullptr) return;
         const int per = (a.seed_n + nblk0 - 1) / nblk0;
@@ -101,7 +96,6 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
         for (int i = i0 + (int)threadIdx.x; i < i1; i += kThreads)
             IO::st_ll(a.seed_dst + i, a.seed_keep ? IO::ld_ll(a.seed_src + i) : 0ll);
     };
-    static_assert(!SYNC::kFlow || XPT > 0, "dataflow GEMV needs register x staging");
     constexpr int EPL = WT_<WT>::EPL;
     constexpr int PK = EPL / 4;                 // float4 packets per 16-B weight load
     static_assert(!(XFIX && EPI == EPI_ATOMIC), "split-K reads an fp32 x");
@@ -156,9 +150,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
 
     // ---- prologue. Issue order matters: vmcnt retires loads in issue order, so x
     // (and gamma) go first, then this wave's first weight batch; the weight stream is
-    // then in flight while x is staged and the norm is reduced. In the dataflow kernel
-    // the weight batch goes first instead (it does not depend on the previous phase)
-    // and x is loaded after the wait.
+    // then in flight while x is staged and the norm is reduced.
     const int g0 = bid * kWavesPerBlock + wave;
     int rows0[ROWS];
     rows_of(g0, rows0);
@@ -169,10 +161,6 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
         // branch-free: clamp the index, load, and predicate only the LDS store
         float4 xv[XPT], gv[XPT];
         longlong2 xf[XFIX ? XPT : 1][2];
-        if constexpr (SYNC::kFlow) {
-            load_batch(w0, rows0, 0);
-            sync.wait();
-        }
 #pragma unroll
         for (int i = 0; i < XPT; ++i) {
             int j = tid + i * kThreads;
@@ -185,7 +173,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
             }
             if (NORM) gv[i] = gamma4<GT>(a.gamma, j);
         }
-        if constexpr (!SYNC::kFlow) load_batch(w0, rows0, 0);
+        load_batch(w0, rows0, 0);
         // RMSNorm (modeling_llama.py:112-117) as gamma*x staged + one scalar rsqrt per
         // dot product in the epilogue: sum_k W[r,k] gamma_k x_k * rstd.
 #pragma unroll

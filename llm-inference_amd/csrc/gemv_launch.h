@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kThreads, min_waves<WT>()) void gemv_kernel(GemvArg
     // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
     WgStamp ts(a.stamps);
-    gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs, NoSync{});
+    gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs);
 }
 
 // Workgroups of one instantiation that fit the chip at once (occupancy x CUs),
