@@ -152,3 +152,35 @@ def test_7b_width_full_context_2048(kv_dtype, path):
     print(f"f7 ctx 2048 kv={'f32' if kv_dtype == _lib.F32 else 'f16'} {path}: logits rel-L2 {r:.3e} "
           f"(vs reference fp32: {rel(logits, f['last_logits']):.3e})")
     assert r < LOGIT_TOL
+
+
+def test_graph_per_split_count_across_chunk_boundaries():
+    """The token graph is captured per active split count (nact = pos // 64 + 1, the
+    host-sized attention / o_proj grids): decode runs that cross 64-position boundaries
+    mid-call (chunks of 37 forwards) replay five different graphs and must equal the
+    eager launches bitwise and the oracle's greedy tokens exactly."""
+    cfg = preset("tiny", max_seq=320)
+    cfg.kv_dtype = _lib.F32
+    f = load("tiny.npz")
+    n_new = 300
+    outs = []
+    for g in (True, False):
+        with Engine(cfg) as e:
+            e.load_synthetic(int(f["seed"]))
+            e.set_prompt(f["prompt"])
+            n_fwd = len(f["prompt"]) + n_new - 1
+            done = 0
+            while done < n_fwd:
+                k = min(37, n_fwd - done)
+                e.decode(k, use_graph=g)
+                done += k
+            outs.append((e.tokens(n_fwd + 1)[len(f["prompt"]):], e.logits()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    o = R.LlamaOracle(R.LlamaConfig(hidden=512, heads=4, kv_heads=4, inter=1024, layers=2, max_seq=320),
+                      seed=int(f["seed"]))
+    otoks, ologits = o.greedy(f["prompt"], n_new)
+    np.testing.assert_array_equal(outs[0][0], otoks)
+    r = rel(outs[0][1], ologits)
+    print(f"nact graphs, {n_new} tokens to ctx {len(f['prompt']) + n_new - 1}: logits rel-L2 {r:.2e}")
+    assert r < LOGIT_TOL
