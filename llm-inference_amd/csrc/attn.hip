@@ -17,7 +17,9 @@
 // read) + 2 * kv_heads * d * sizeof(cache) (current slot write); attn_oproj adds
 // hidden * heads * d * sizeof(W) (the o_proj weights).
 //
-// Work split (MI355X): grid (heads, max_seq / 64). A workgroup (256 threads = 16
+// Work split (MI355X): grid (heads, active splits ceil(ctx / 64)) when the caller knows
+// the position on the host (the engine: one token graph per split count), else
+// (heads, max_seq / 64) with the inactive splits exiting. A workgroup (256 threads = 16
 // groups of 16 lanes) owns 64 cached positions of one head; a 16-lane group reads a
 // 256-byte fp16 K/V row with one 16-B load per lane (4 rows per wave instruction),
 // all its rows issued before anything waits. 32 heads alone would use 32 of 256 CUs;
