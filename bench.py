@@ -9,8 +9,11 @@ workload: synthetic random-init Llama-2-7B weights (llmi-prng-v1, fp16), an
 8-token synthetic prompt, then single-token decode forwards at positions
 0..2047 (ctx 1..2048; 2048 forwards, 2041 generated tokens), all inside the
 native engine (one hipGraph replay per token). N > 1 runs tensor parallel over
-N GPUs (config 4: head/FFN row/col shard + RCCL all-reduce); each rank streams
-1/N of the weights, total work is fixed ("strong" scaling).
+N GPUs (config 4: head/FFN row/col shard; the per-layer residual exchange is the
+one-shot peer exchange over xGMI once it has matched RCCL's tokens on a short
+run, else RCCL all-reduce); each rank streams 1/N of the weights, total work is
+fixed ("strong" scaling). Started without a launcher, `--gpus N` spawns the N
+rank processes itself (before any GPU call).
 
 value = generated tokens / s (whole job). Also reported: HBM roofline of the
 dominant kernel (gate_up GEMV, HIP events on the engine stream, launches cycling
@@ -110,6 +113,8 @@ def cpu_baseline(sample_layers: int = 2, n_short: int = 12, n_long: int = 6, lon
     l_mean = l_short + slope * ((MAX_SEQ + 1) / 2 - c_short)   # mean layer time over ctx 1..2048
     per_tok = t_head + 32 * l_mean
     out = {"value": round(1.0 / per_tok, 4), "unit": "tokens/s", "cores": int(threads), "kind": "port",
+           "threads_note": "BLAS threads = the box's per-GPU CPU share (OMP_NUM_THREADS is pinned to 16 there; "
+                           "os.cpu_count() reports the whole host)",
            **cpu_info(), "ctx": f"1..{MAX_SEQ} (modelled from samples at ctx 1..{n_short} and "
                                  f"{long_ctx + 1}..{long_ctx + n_long})",
            "sample": f"numpy oracle (oracle/llama_ref.py, fp32 weights from the fp16 PRNG values), Llama-2-7B "
@@ -221,7 +226,39 @@ def int8_side(n_new: int = MAX_SEQ - PROMPT + 1):
             "gate_up_GBps": round(gu_b / (gu_us * 1e-6) / 1e9, 1)}
 
 
-def tp_exchange_side(eng, layers, ms_per_token, wbytes):
+def open_oneshot_exchange(eng, dist, prompt, world, n_check: int = 64):
+    """Config 4's exchange: every rank maps every peer's inbox (IPC handles all-gathered
+    over gloo), then a short greedy run over RCCL and over the one-shot peer exchange must
+    give the same tokens on every rank before the one-shot path is used for the timed run;
+    otherwise (or on any error, e.g. a peer that never arrives: error bit 8, no hang) the
+    run stays on RCCL and the JSON line says why."""
+    info = {"mode": "rccl"}
+    ok, why = False, ""
+    try:
+        hs = [None] * world
+        dist.all_gather_object(hs, eng.xchg_handle())
+        eng.xchg_open(hs)
+        ta = eng.generate(prompt, n_check)
+        eng.set_exchange(1)
+        tb = eng.generate(prompt, n_check)
+        ok = bool((ta == tb).all())
+        why = "" if ok else "one-shot tokens differ from RCCL"
+    except Exception as e:  # reported, never fatal: RCCL carries the run
+        why = repr(e)[:300]
+    oks = [None] * world
+    dist.all_gather_object(oks, (ok, why))
+    if all(o[0] for o in oks):
+        info["mode"] = "oneshot"
+    else:
+        try:
+            eng.set_exchange(0)
+        except Exception:
+            pass
+        info["oneshot_rejected"] = [o[1] for o in oks if not o[0]][:2]
+    return info
+
+
+def tp_exchange_side(eng, layers, ms_per_token, wbytes, mode="rccl"):
     """TP exchange budget: per token 2 * layers int64 all-reduces of the
     hidden-size fixed-point residual (32 KB) plus one uint64 max over the lm_head
     partials. Times the engine's own residual all-reduce on its RCCL communicator --
@@ -229,14 +266,74 @@ def tp_exchange_side(eng, layers, ms_per_token, wbytes):
     collective: every rank runs this) -- and sets calls x latency against the measured
     ms per token and the per-rank weight stream."""
     out = {"calls_per_token": 2 * layers + 1, "payload_bytes": 4096 * 8}
+    out["mode"] = mode
     out["allreduce_us_eager"] = round(eng.time_kernel("allreduce", iters=200)[0], 2)
     out["allreduce_us_graph"] = round(eng.time_kernel("allreduce_graph", iters=256)[0], 2)
     lat = out["allreduce_us_graph"]
+    if mode == "oneshot":
+        out["oneshot_us_eager"] = round(eng.time_kernel("xchg", iters=200)[0], 2)
+        out["oneshot_us_graph"] = round(eng.time_kernel("xchg_graph", iters=256)[0], 2)
+        lat = out["oneshot_us_graph"]
     out["exchange_us_per_token_est"] = round(lat * out["calls_per_token"], 1)
     out["ms_per_token"] = round(ms_per_token, 4)
     out["weight_stream_us_per_token_at_6.2TBps"] = round(wbytes / 6.2e12 * 1e6, 1)
     out["exchange_share_of_token"] = round(out["exchange_us_per_token_est"] / (ms_per_token * 1e3), 3)
     return out
+
+
+def spawn_workers(n: int, argv) -> int:
+    """`--gpus N` (N > 1) started without a launcher: start N workers of this script,
+    one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), and
+    relay rank 0's JSON line. The parent itself never imports the engine library or
+    touches a GPU; if any worker fails, the others are stopped and its code returned."""
+    import socket
+    import subprocess
+    import tempfile
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL))
+    progress(f"spawned {n} workers (rendezvous 127.0.0.1:{port})")
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+        if rc == 0 and p.returncode != 0:
+            rc = p.returncode
+    out0.seek(0)
+    for line in out0.read().splitlines():  # the JSON line to stdout, library chatter to stderr
+        print(line, file=sys.stdout if line.startswith("{") else sys.stderr, flush=True)
+    return rc
+
+
+def dry_run(rank: int, world: int):
+    """Launcher check: the rendezvous and the gloo group, no GPU, no engine."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                       "pid": os.getpid()})
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        ranks = [{"rank": 0, "local_rank": 0, "pid": os.getpid()}]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks}), flush=True)
 
 
 def main():
@@ -254,13 +351,20 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch kernels eagerly instead of replaying the hipGraph (profiling: rocprofv3 "
                          "kernel tracing of graph replays crashes on ROCm 7.2)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="check the launcher only: spawn / rendezvous / gloo group, then exit before any GPU call")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_workers(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dry_run(rank, world)
+        return
 
     import llmi
     from llmi.engine import Engine, preset, synth_prompt, tp_unique_id
@@ -287,6 +391,12 @@ def main():
     def barrier():
         if dist is not None:
             dist.barrier()
+
+    xchg = {"mode": "rccl" if tp_id is not None else "none"}
+    if dist is not None and os.environ.get("LLMI_TP_EXCHANGE", "oneshot") == "oneshot":
+        progress("one-shot peer exchange: open + check against RCCL")
+        xchg = open_oneshot_exchange(eng, dist, prompt, world)
+        progress(f"tp exchange: {xchg}")
 
     def one_generation():
         eng.set_prompt(prompt)
@@ -327,7 +437,10 @@ def main():
     if tp_id is not None:
         progress("tp exchange side measurement")
         try:
-            side["tp_exchange"] = tp_exchange_side(eng, cfg.layers, elapsed * 1e3 / args.steps / n_fwd, wbytes)
+            side["tp_exchange"] = tp_exchange_side(eng, cfg.layers, elapsed * 1e3 / args.steps / n_fwd, wbytes,
+                                                   mode=xchg["mode"])
+            if "oneshot_rejected" in xchg:
+                side["tp_exchange"]["oneshot_rejected"] = xchg["oneshot_rejected"]
         except Exception as e:  # reported, never fatal to the GPU number
             side["tp_exchange"] = {"error": repr(e)[:300]}
     if world == 1 and not args.no_side:

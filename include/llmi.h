@@ -259,9 +259,10 @@ int llmi_tp_allreduce(llmi_tp_comm* comm, void* buf, size_t count, int dtype, ll
 int llmi_tp_comm_destroy(llmi_tp_comm* comm);
 
 /* device: HIP device ordinal. tp_id: 128-byte RCCL id (llmi_tp_unique_id, broadcast
- * to every rank); required when tp_world > 1. With tp_world == 1 it may be NULL (no
- * communicator) or an id: the engine then creates a one-rank communicator and runs
- * the same RCCL all-reduces inside the token graph as a TP rank does (identities). */
+ * to every rank): the engine creates an RCCL communicator and the token graph all-reduces
+ * over it (with tp_world == 1 too: identities). With tp_world > 1 and tp_id NULL there is
+ * no RCCL communicator: the ranks must open the one-shot peer exchange (below) before
+ * they decode. */
 int llmi_engine_create(const llmi_config* cfg, int device, const void* tp_id, llmi_engine** out);
 int llmi_engine_destroy(llmi_engine* e);
 /* Llama<T>::loadWeightsFromDummy (src/models/llama/llama.h) with llmi-prng-v1 weights. */
@@ -318,11 +319,31 @@ llmi_stream_t llmi_engine_stream(llmi_engine* e);
  * rank must make the same call.
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
+/* which 8 / 9: the same residual exchange over the one-shot peer path (below), eager /
+ * graph-replayed -- also a collective. */
+
+/* ---- One-shot peer exchange for tensor parallel decode (config 4; replaces the RCCL
+ * all-reduces of the token graph: the sum of the row-parallel partials of
+ * modeling_llama.py's pretraining_tp, :251-266 / :443-446, and the argmax-key max).
+ * Every rank owns an inbox in its HBM; each exchange is ONE kernel that writes this rank's
+ * int64 partial into every peer's inbox over xGMI, raises per-slice flags, waits for every
+ * rank's flags and sums the slots in rank order (exact: bitwise the RCCL result).
+ *   1. llmi_engine_xchg_handle: allocate the inbox, return its 64-byte IPC handle;
+ *   2. the launcher all-gathers the handles (any side channel; rank order);
+ *   3. llmi_engine_xchg_open(e, handles[world * 64]): map every peer's inbox;
+ *   4. llmi_engine_set_exchange(e, 1) (0 = RCCL again; graphs are re-captured).
+ * A peer that never arrives (2 s) sets error bit 8: llmi_engine_tokens fails, no hang. */
+int llmi_engine_xchg_handle(llmi_engine* e, void* out64);
+int llmi_engine_xchg_open(llmi_engine* e, const void* handles);
+int llmi_engine_set_exchange(llmi_engine* e, int mode);
 /* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built
  * afterwards) write a per-workgroup timeline into dev_buf (8 x uint64 per
  * workgroup at 8 * linear block id: start, two kernel-defined marks, end, CU id;
  * 100 MHz clock). NULL switches it off. */
 int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf);
+/* Test hook: overwrite the device decode state's next position only (the host's copy is
+ * left alone), to check that a host/device position mismatch is reported (error bit 4). */
+int llmi_engine_debug_set_next_pos(llmi_engine* e, int next_pos);
 
 /* ---- In-process tensor-parallel group (no reference counterpart: the
  * reference has no TP). W rank engines with tp_rank 0..W-1 on ONE device and
@@ -343,6 +364,10 @@ int llmi_group_tokens(llmi_group* g, int rank, int32_t* out, int n, int* n_valid
 /* last logits over the full vocab: the ranks' slices concatenated */
 int llmi_group_logits(llmi_group* g, float* out, int n);
 int llmi_group_hidden(llmi_group* g, int rank, float* out, int n);
+/* mode 0: the in-place reduction kernel; 1: the one-shot peer exchange's kernels (every
+ * rank's push, then every rank's wait + rank-order reduce; the ranks' inboxes are the
+ * group's own device buffers) -- the single-GPU parity check of that protocol. */
+int llmi_group_set_exchange(llmi_group* g, int mode);
 
 #ifdef __cplusplus
 }

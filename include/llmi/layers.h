@@ -52,6 +52,48 @@ public:
     }
 };
 
+namespace llmi_detail {
+// The layers compute in fp32 (fp32 activations keep the logits within 1e-3 of the
+// reference). An activation of the reference's fp16 instantiation
+// (TensorWrapper<half>, self_decoder.cpp:59-81 with T = half) is staged: converted into
+// an fp32 buffer on entry (load) and rounded back to fp16 by store(); an FP32 tensor is
+// used in place; any other dtype is an error.
+class ActF32 {
+public:
+    ActF32(Tensor* t, BaseAllocator* alloc, void* stream, bool load, const char* what)
+        : t_(t), alloc_(alloc), stream_(stream) {
+        LLM_CHECK_WITH_INFO(t && (t->dtype == FP32 || t->dtype == FP16),
+                            std::string(what) + ": activations must be FP32 or FP16 tensors");
+        if (t->dtype == FP32) {
+            view_ = t->as<float>();
+            return;
+        }
+        const size_t n = (size_t)t->size();
+        buf_ = alloc->Malloc(buf_, n * sizeof(float), false);
+        own_ = std::make_unique<TensorWrapper<float>>(t->location, FP32, t->shape, buf_);
+        view_ = own_.get();
+        if (load) LLMI_CALL(llmi_convert(t->as<half_t>()->data, LLMI_F16, buf_, LLMI_F32, n, stream));
+    }
+    ActF32(const ActF32&) = delete;
+    ActF32& operator=(const ActF32&) = delete;
+    ~ActF32() {
+        if (buf_) alloc_->Free(buf_, false);
+    }
+    TensorWrapper<float>* get() const { return view_; }
+    void store() {  // fp16 output: the fp32 result rounded back (RNE)
+        if (own_) LLMI_CALL(llmi_convert(buf_, LLMI_F32, t_->as<half_t>()->data, LLMI_F16, (size_t)t_->size(), stream_));
+    }
+
+private:
+    Tensor* t_;
+    BaseAllocator* alloc_;
+    void* stream_;
+    float* buf_ = nullptr;
+    std::unique_ptr<TensorWrapper<float>> own_;
+    TensorWrapper<float>* view_ = nullptr;
+};
+}  // namespace llmi_detail
+
 // --------------------------------------------------------------- weights
 template <typename T>
 class LlamaLayerWeight {
@@ -163,8 +205,10 @@ private:
     void ForwardCache(TensorMap& inputs, TensorMap& outputs, LLaMAattentionWeights<T>& weights,
                       LLaMAAttentionDynParams& params) {
         allocForForward(params);
-        TensorWrapper<float>* attention_input = inputs["attention_input"]->as<float>();
-        TensorWrapper<float>* attention_output = outputs["attention_output"]->as<float>();
+        llmi_detail::ActF32 in(inputs["attention_input"], allocator, stream, true, "LLaMASelfAttentionLayer");
+        llmi_detail::ActF32 out(outputs["attention_output"], allocator, stream, false, "LLaMASelfAttentionLayer");
+        TensorWrapper<float>* attention_input = in.get();
+        TensorWrapper<float>* attention_output = out.get();
         TensorWrapper<CT>* key_cache = outputs["all_k_cache"]->as<CT>();
         TensorWrapper<CT>* value_cache = outputs["all_v_cache"]->as<CT>();
         TensorWrapper<bool>* finished = inputs["finished"]->as<bool>();
@@ -177,6 +221,7 @@ private:
                                mha_output.get(), attn_static_params, stream);
         launchLinearGemm(mha_output.get(), weights.output, attention_output, cublas_wrapper ? cublas_wrapper : &cw,
                          false, true);
+        out.store();
     }
 
     int head_num, kv_head_num, head_size, hidden;
@@ -219,13 +264,14 @@ public:
     // ffn.cpp:52-93: gate_up GEMV -> SiLU*mul -> down GEMV
     void forward(TensorMap& inputs, TensorMap& outputs, LLaMAFFNWeights<T>& weights, LLaMAAttentionDynParams& params) {
         allocForForward(params.is_ctx ? params.num_tokens : params.batch_size);
-        TensorWrapper<float>* ffn_input = inputs["ffn_input"]->as<float>();
-        TensorWrapper<float>* ffn_output = outputs["ffn_output"]->as<float>();
+        llmi_detail::ActF32 in(inputs["ffn_input"], allocator, stream, true, "LLaMAFFNLayer");
+        llmi_detail::ActF32 out(outputs["ffn_output"], allocator, stream, false, "LLaMAFFNLayer");
         cublasWrapper cw{stream};
         cublasWrapper* c = cublas_wrapper ? cublas_wrapper : &cw;
-        launchLinearGemm(ffn_input, weights.gateAndup, SwiGLU_input.get(), c, false, true);
+        launchLinearGemm(in.get(), weights.gateAndup, SwiGLU_input.get(), c, false, true);
         launchAct(SwiGLU_input.get(), down_proj_input.get(), stream);
-        launchLinearGemm(down_proj_input.get(), weights.down, ffn_output, c, false, true);
+        launchLinearGemm(down_proj_input.get(), weights.down, out.get(), c, false, true);
+        out.store();
     }
 
 private:
@@ -263,8 +309,11 @@ public:
             decoder_residual = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{dyn_params.batch_size, hidden}, resid_ptr);
         }
         dyn_params.is_ctx = false;  // one token: FFN scratch is batch_size rows
-        TensorWrapper<float>* decoder_input = input_tensors["decoder_input"]->as<float>();
-        TensorWrapper<float>* decoder_output = output_tensors["decoder_output"]->as<float>();
+        // fp16 activations (Llama<half>) are staged once here; the sublayers then run fp32
+        llmi_detail::ActF32 din(input_tensors["decoder_input"], allocator, stream, true, "LlamaSelfDecoder");
+        llmi_detail::ActF32 dout(output_tensors["decoder_output"], allocator, stream, false, "LlamaSelfDecoder");
+        TensorWrapper<float>* decoder_input = din.get();
+        TensorWrapper<float>* decoder_output = dout.get();
         int layer = 0;
         TensorWrapper<int> layer_id(CPU, INT32, {1}, &layer);
         TensorMap attn_in{{"attention_input", decoder_input}, {"finished", input_tensors["finished"]},
@@ -286,6 +335,7 @@ public:
             decoder_input = decoder_output;
             attn_in.insert("attention_input", decoder_output);
         }
+        dout.store();
     }
 
 private:
@@ -356,8 +406,10 @@ public:
         TensorWrapper<int>* layer_id = inputs["layer_id"]->as<int>();
         TensorWrapper<float>* all_k_cache = outputs["all_k_cache"]->as<float>();
         TensorWrapper<float>* all_v_cache = outputs["all_v_cache"]->as<float>();
+        llmi_detail::ActF32 in(inputs["attention_input"], allocator, stream, true, "LLaMAContextAttentionLayer");
+        llmi_detail::ActF32 out(outputs["attention_output"], allocator, stream, false, "LLaMAContextAttentionLayer");
         // 1. qkv linear
-        launchLinearGemm(inputs["attention_input"]->as<float>(), weights.qkv, qkv_buf_wo_pad, c, false, true);
+        launchLinearGemm(in.get(), weights.qkv, qkv_buf_wo_pad, c, false, true);
         // 2. RoPE (position history + s) and [num_tokens, ...] -> [bs, heads, max_q_len, head]
         launchAddFusedQKVBiasTransposeAndRoPE(q_buf_w_pad, k_buf_w_pad, v_buf_w_pad, qkv_buf_wo_pad, weights.qkv,
                                               padding_offset, history_length, input_length, static_params, stream);
@@ -371,7 +423,8 @@ public:
         launchLinearStridedBatchGemm(qk_buf, v_cache_buf, qkv_buf_w_pad, c, false, false);
         // 5. [bs, heads, max_q_len, head] -> [num_tokens, H], then o_proj
         launchTransposeOutRemovePadding(qkv_buf_w_pad, padding_offset, qkv_buf_wo_pad_1, stream);
-        launchLinearGemm(qkv_buf_wo_pad_1, weights.output, outputs["attention_output"]->as<float>(), c, false, true);
+        launchLinearGemm(qkv_buf_wo_pad_1, weights.output, out.get(), c, false, true);
+        out.store();
         freeBuf();
     }
 
@@ -440,10 +493,12 @@ public:
         launchCalPaddingoffset(padding_offset.get(), cum_seqlens.get(), seq_lens->as<int>(), stream);
         launchBuildCausalMasks(attention_mask.get(), seq_lens->as<int>(), input_tensors["context_length"]->as<int>(),
                                stream);
-        TensorWrapper<float>* decoder_output = output_tensors["decoder_output"]->as<float>();
+        llmi_detail::ActF32 din(input_tensors["decoder_input"], allocator, stream, true, "LlamaContextDecoder");
+        llmi_detail::ActF32 dout(output_tensors["decoder_output"], allocator, stream, false, "LlamaContextDecoder");
+        TensorWrapper<float>* decoder_output = dout.get();
         int layer = 0;
         TensorWrapper<int> layer_id(CPU, INT32, {1}, &layer);
-        TensorMap ctx_attn_inputs{{"attention_input", input_tensors["decoder_input"]},
+        TensorMap ctx_attn_inputs{{"attention_input", din.get()},
                                   {"padding_offset", padding_offset.get()},
                                   {"history_length", input_tensors["history_length"]},
                                   {"input_length", seq_lens},
@@ -468,6 +523,7 @@ public:
             launchAddResidual(decoder_residual.get(), decoder_output, false, stream);
             ctx_attn_inputs.insert("attention_input", decoder_output);
         }
+        dout.store();
         freeBuf();
     }
 

@@ -77,7 +77,13 @@ struct Tensor {
     virtual int size() const {
         return shape.empty() ? 0 : std::accumulate(shape.begin(), shape.end(), 1, std::multiplies<int>());
     }
-    template <typename T> TensorWrapper<T>* as() { return static_cast<TensorWrapper<T>*>(this); }
+    // the reference's as<T>() is an unchecked static_cast (tensor.h:63-66); a view of the
+    // wrong element type would be read silently as another type, so it is checked here
+    template <typename T> TensorWrapper<T>* as() {
+        LLM_CHECK_WITH_INFO(getTensorType<T>() == dtype, "Tensor::as<T>(): the tensor's dtype (" + std::to_string(dtype) +
+                                                             ") is not T (" + std::to_string(getTensorType<T>()) + ")");
+        return static_cast<TensorWrapper<T>*>(this);
+    }
     std::string DeviceString() const { return location == GPU ? "GPU" : location == CPU ? "CPU" : "CPU_PINNED"; }
     virtual std::string toString() const {
         std::ostringstream os;

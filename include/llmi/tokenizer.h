@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <queue>
 #include <stdexcept>
 #include <string>
@@ -28,29 +29,42 @@ public:
     // length-prefixed strings; vocabulary: count, then per piece {len, len ints
     // (one byte each), id, float score}.
     void Initialize(std::string file) {
-        std::FILE* f = std::fopen(file.c_str(), "rb");
+        // the file is external data: every count, length and id is range-checked, a short
+        // read stops the parse at once, and the FILE* is closed on every path
+        std::unique_ptr<std::FILE, int (*)(std::FILE*)> f(std::fopen(file.c_str(), "rb"), &std::fclose);
         if (!f) throw std::runtime_error("[oneLLM][ERROR] Tokenizer: cannot open " + file);
-        Reader r{f};
-        const int version = r.i32();
+        auto bad = [&](const std::string& why) {
+            return std::runtime_error("[oneLLM][ERROR] Tokenizer: " + why + " in " + file);
+        };
+        Reader r{f.get()};
+        auto i32 = [&](const char* what) {
+            const int v = r.i32();
+            if (!r.ok) throw bad(std::string("truncated file (reading ") + what + ")");
+            return v;
+        };
+        const int version = i32("version");
         if (version >= 1) {
-            const int kv = r.i32();
+            const int kv = i32("metadata count");
+            if (kv < 0 || kv > kMaxCount) throw bad("metadata count out of range");
             for (int i = 0; i < kv; ++i) {
-                std::string key = r.str(), value = r.str();
+                std::string key = r.str(kMaxPiece), value = r.str(kMaxPiece);
+                if (!r.ok) throw bad("truncated or oversized metadata entry");
                 meta_[key] = value;
             }
         }
-        const int n = r.i32();
-        if (n <= 0) throw std::runtime_error("[oneLLM][ERROR] Tokenizer: empty vocabulary in " + file);
+        const int n = i32("vocabulary count");
+        if (n <= 0 || n > kMaxCount) throw bad("vocabulary count out of range");
         for (int i = 0; i < n; ++i) {
-            const int len = r.i32();
+            const int len = i32("piece length");
+            if (len < 0 || len > kMaxPiece) throw bad("piece length out of range");
             std::string piece(len, '\0');
-            for (int j = 0; j < len; ++j) piece[j] = (char)(uint8_t)r.i32();
-            const int id = r.i32();
+            for (int j = 0; j < len; ++j) piece[j] = (char)(uint8_t)i32("piece byte");
+            const int id = i32("piece id");
+            if (id < 0 || id >= kMaxCount) throw bad("piece id out of range");
             const float score = r.f32();
+            if (!r.ok) throw bad("truncated file (reading piece score)");
             add_piece(piece, id, score);
         }
-        std::fclose(f);
-        if (!r.ok) throw std::runtime_error("[oneLLM][ERROR] Tokenizer: truncated file " + file);
     }
 
     std::vector<int> Encode(const std::string& ori) const {
@@ -161,6 +175,8 @@ public:
 
 private:
     static constexpr int kNoFix = -999999;
+    static constexpr int kMaxPiece = 1024;     // bytes per piece / metadata string
+    static constexpr int kMaxCount = 1 << 24;  // pieces, metadata entries, ids
     struct Sym {
         int pos, len, fix;
         bool unk;  // a byte that starts no piece: emitted as its <0xXX> byte piece
@@ -184,10 +200,14 @@ private:
             ok = ok && std::fread(&v, 4, 1, f) == 1;
             return v;
         }
-        std::string str() {
+        std::string str(int max_len) {
             const int len = i32();
-            std::string s(len > 0 ? len : 0, '\0');
-            if (len > 0) ok = ok && std::fread(&s[0], 1, len, f) == (size_t)len;
+            if (!ok || len < 0 || len > max_len) {
+                ok = false;
+                return std::string();
+            }
+            std::string s(len, '\0');
+            if (len > 0) ok = std::fread(&s[0], 1, len, f) == (size_t)len;
             return s;
         }
     };

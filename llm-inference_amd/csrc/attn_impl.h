@@ -215,6 +215,15 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     }
 
     if (pos < 0 || pos >= a.max_seq) return;  // host validates; guard against a stale state
+    if constexpr (HOST_SIZED) {
+        // the grid (and the o_proj's merge count) came from the host's position: if the
+        // device state disagrees, keys past nact * CH would be dropped or stale partials
+        // merged -- report it (tokens_out raises) instead of computing a wrong token
+        if (pos / CH + 1 != (int)gridDim.y) {
+            if (a.err != nullptr && tid == 0 && split == 0) atomicOr(a.err, 4);
+            return;
+        }
+    }
     const int ctx = pos + 1;
     if (start >= ctx) return;
     const int end = min(start + CH, ctx);

@@ -49,6 +49,16 @@ namespace {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace
 
+// GEMV grid overrides for A/B builds (0 = gemv_grid's automatic choice)
+#ifndef LLMI_QKV_GRID
+#define LLMI_QKV_GRID 0
+#endif
+#ifndef LLMI_GU_GRID
+#define LLMI_GU_GRID 0
+#endif
+#ifndef LLMI_DOWN_GRID
+#define LLMI_DOWN_GRID 0
+#endif
 #ifndef LLMI_I8_DOWN_KSPLIT
 #define LLMI_I8_DOWN_KSPLIT 4  // int8 down K slices: 13B down 18.2 -> 16.5 us, 8-layer loop 682 -> 665 us (A/B)
 #endif
@@ -136,6 +146,15 @@ struct Engine {
     StepGraphs graphs;
     int rec_nact = 0;  // active split count the next recorded step's attention is sized for
     ncclComm_t comm = nullptr;
+    // one-shot peer exchange (xchg.hip): this rank's inbox (uncached HBM), every rank's
+    // inbox base (IPC-mapped for peers) in device memory, per-slice epoch counters.
+    // xchg_mode 1 replaces the RCCL all-reduces of the token graph (RCCL stays selectable).
+    int xchg_mode = 0;
+    char* inbox = nullptr;
+    char** peers_dev = nullptr;
+    unsigned long long* xchg_ep = nullptr;
+    std::vector<void*> peers_opened;  // IPC mappings to close
+    int xchg_cap_n = 0;
     // prefill scratch (allocated on first use): rows of one prefill chunk
     char* pf = nullptr;
     int pf_rows = 0;
@@ -162,6 +181,10 @@ struct Engine {
         if (samp_vals) (void)hipFree(samp_vals);
         graphs.clear();
         if (comm) (void)ncclCommDestroy(comm);
+        for (void* p : peers_opened) (void)hipIpcCloseMemHandle(p);
+        if (inbox) (void)hipFree(inbox);
+        if (peers_dev) (void)hipFree(peers_dev);
+        if (xchg_ep) (void)hipFree(xchg_ep);
         if (wblob) (void)hipFree(wblob);
         if (kcache) (void)hipFree(kcache);
         if (vcache) (void)hipFree(vcache);
@@ -209,8 +232,9 @@ struct Engine {
         }
         // a communicator whenever an id is given -- also at tp_world 1, where the
         // all-reduces are identities but still run (captured in the token graph)
-        if (!grouped && (W > 1 || tp_id != nullptr)) {
-            LLMI_REQUIRE(tp_id != nullptr, "engine: tp_world > 1 needs the RCCL unique id");
+        // tp_world > 1 without an id: no RCCL; the ranks must open the one-shot peer
+        // exchange (llmi_engine_xchg_open) before they decode
+        if (!grouped && tp_id != nullptr) {
             ncclUniqueId id;
             std::memcpy(&id, tp_id, sizeof(id));
             ncclResult_t r = ncclCommInitRank(&comm, W, id, c.tp_rank);
@@ -540,6 +564,7 @@ struct Engine {
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
+        a.grid = LLMI_QKV_GRID;
         return a;
     }
     AttnArgs attn_args(int l) const {
@@ -561,6 +586,7 @@ struct Engine {
         a.hidden = c.hidden;
         a.out = attn_out; a.workspace = attn_ws;
         a.nact = rec_nact;
+        a.err = &st->error;
         return a;
     }
     OprojArgs o_args(int l) const {
@@ -588,6 +614,7 @@ struct Engine {
         a.seed_keep = c.tp_rank == 0 ? 1 : 0;
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
+        a.grid = LLMI_GU_GRID;
         return a;
     }
     GemvArgs down_args(int l) const {
@@ -600,6 +627,7 @@ struct Engine {
         // int8 rows are half the bytes of fp16 ones: K slices keep the loads per row in
         // flight and the x image per workgroup small (exact: int64 atomics)
         a.ksplit = (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT : 1;
+        a.grid = LLMI_DOWN_GRID;
         return a;
     }
 
@@ -628,6 +656,63 @@ struct Engine {
         return sample_pick_launch(st, samp_ids, samp_vals, sample_k, sample_seed, partials, lm_grid, stream);
     }
 
+    // ------------------------------------------------- TP exchange (config 4)
+    // The per-token collectives: int64 sum of the residual partials (op 0) or uint64 max of
+    // the argmax keys (op 2), over RCCL or the one-shot peer exchange.
+    int alloc_xchg() {
+        if (inbox) return LLMI_OK;
+        const int W = c.tp_world;
+        xchg_cap_n = std::max(c.hidden, lm_grid);
+        xchg_cap_n += xchg_cap_n & 1;
+        LLMI_REQUIRE(xchg_cap_n <= kXchgSlice * kXchgMaxSlices, "xchg: hidden / lm_head partials exceed the inbox");
+        const size_t bytes = xchg_inbox_bytes(W, xchg_cap_n);
+        LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&inbox), bytes, hipDeviceMallocUncached));
+        LLMI_HIP(hipMemset(inbox, 0, bytes));
+        LLMI_HIP(hipMalloc(&xchg_ep, kXchgMaxSlices * sizeof(unsigned long long)));
+        LLMI_HIP(hipMemset(xchg_ep, 0, kXchgMaxSlices * sizeof(unsigned long long)));
+        LLMI_HIP(hipMalloc(&peers_dev, (size_t)W * sizeof(char*)));
+        return LLMI_OK;
+    }
+    // every rank's inbox base, in rank order (peers[rank] must be this rank's own inbox)
+    int set_peers(const std::vector<char*>& p) {
+        LLMI_REQUIRE((int)p.size() == c.tp_world && p[c.tp_rank] == inbox, "xchg: bad peer table");
+        LLMI_HIP(hipMemcpy(peers_dev, p.data(), p.size() * sizeof(char*), hipMemcpyHostToDevice));
+        return LLMI_OK;
+    }
+    XchgArgs xchg_args(void* buf, int n, int op, int mode) const {
+        XchgArgs a;
+        a.buf = static_cast<long long*>(buf);
+        a.n = n;
+        a.op = op;
+        a.rank = c.tp_rank;
+        a.world = c.tp_world;
+        a.peers = peers_dev;
+        a.ep = xchg_ep;
+        a.err = &st->error;
+        a.mode = mode;
+        a.cap_n = xchg_cap_n;
+        a.cap_w = c.tp_world;
+        return a;
+    }
+    int exchange(void* buf, int n, int op) {
+        if (xchg_mode == 1) return xchg_launch(xchg_args(buf, n, op, 3), stream);
+        if (!comm) return LLMI_OK;
+        const ncclResult_t r = op == 0 ? ncclAllReduce(buf, buf, n, ncclInt64, ncclSum, comm, stream)
+                                       : ncclAllReduce(buf, buf, n, ncclUint64, ncclMax, comm, stream);
+        LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        return LLMI_OK;
+    }
+    int set_exchange(int mode) {
+        LLMI_REQUIRE(mode == 0 || mode == 1, "set_exchange: mode must be 0 (RCCL) or 1 (one-shot peer exchange)");
+        LLMI_REQUIRE(!grouped, "set_exchange: a group rank's exchange is its group's");
+        LLMI_REQUIRE(mode == 0 || (inbox && peers_ready), "set_exchange: open the peer exchange first (xchg_open)");
+        LLMI_HIP(hipStreamSynchronize(stream));
+        graphs.clear();  // the captured steps change
+        xchg_mode = mode;
+        return LLMI_OK;
+    }
+    bool peers_ready = false;
+
     int set_sampling(int k, uint64_t sd) {
         LLMI_REQUIRE(k >= 0 && k <= 16, "set_sampling: k must be in [0, 16] (0 = greedy)");
         LLMI_REQUIRE(k == 0 || (c.tp_world == 1 && !grouped), "set_sampling: sampling needs the full logits (tp_world 1)");
@@ -649,23 +734,12 @@ struct Engine {
         LLMI_TRY(rec_start());
         for (int l = 0; l < c.layers; ++l) {
             LLMI_TRY(rec_attn(l));
-            if (comm) {  // exact int64 sum of the fixed-point residual partials
-                ncclResult_t r = ncclAllReduce(xacc, xacc, c.hidden, ncclInt64, ncclSum, comm, stream);
-                LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
-            }
+            LLMI_TRY(exchange(xacc, c.hidden, 0));  // exact int64 sum of the fixed-point residual partials
             LLMI_TRY(rec_ffn(l));
-            if (comm) {  // exact int64 sum of the layer outputs (rank 0 carried the residual)
-                ncclResult_t r = ncclAllReduce(res[(l + 1) % 2], res[(l + 1) % 2], c.hidden, ncclInt64, ncclSum,
-                                               comm, stream);
-                LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
-            }
+            LLMI_TRY(exchange(res[(l + 1) % 2], c.hidden, 0));  // layer output (rank 0 carried the residual)
         }
         LLMI_TRY(rec_head());
-        if (comm) {
-            ncclResult_t r = ncclAllReduce(partials, partials, lm_grid, ncclUint64, ncclMax, comm, stream);
-            LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(max): ") + ncclGetErrorString(r));
-        }
-        return LLMI_OK;
+        return exchange(partials, lm_grid, 2);  // max of the vocab-parallel argmax keys
     }
 
     static int nact_of(int pos) { return pos / kAttnChunk + 1; }
@@ -695,6 +769,8 @@ struct Engine {
 
     int decode(int n, int use_graph) {
         LLMI_REQUIRE(prompt_len > 0, "decode: set_prompt first");
+        LLMI_REQUIRE(c.tp_world == 1 || comm || xchg_mode == 1,
+                     "decode: tp_world > 1 needs an RCCL id at create or the one-shot exchange (xchg_open + set_exchange)");
         LLMI_REQUIRE(n >= 0 && host_next_pos + n <= c.max_seq, "decode: would run past max_seq");
         if (use_graph && n > 0)  // every graph this run replays, captured before the first launch
             for (int k = nact_of(host_next_pos); k <= nact_of(host_next_pos + n - 1); ++k) LLMI_TRY(build_graph(k));
@@ -903,7 +979,7 @@ struct Engine {
         DecodeState h;
         LLMI_HIP(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
         LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error) +
-                                       " (1: token id out of range, 2: position overflow)");
+                                       " (1: token id out of range, 2: position overflow, 4: attention split count != device position)");
         const int m = n < valid ? n : valid;
         if (m > 0) LLMI_HIP(hipMemcpy(out, tokens, (size_t)m * 4, hipMemcpyDeviceToHost));
         if (n_valid) *n_valid = valid;
@@ -922,6 +998,9 @@ struct Group {
     hipStream_t stream = nullptr;
     void** ptrs = nullptr;  // device [4][W]: xacc, res[0], res[1], partials of every rank
     StepGraphs graphs;
+    // 0: group_reduce_kernel; 1: the one-shot peer exchange's kernels (xchg.hip) -- every
+    // rank's push, then every rank's reduce (one stream: the waits find their flags set)
+    int xchg_mode = 0;
 
     ~Group() {
         graphs.clear();
@@ -953,19 +1032,46 @@ struct Group {
         return LLMI_OK;
     }
 
+    int set_exchange(int mode) {
+        LLMI_REQUIRE(mode == 0 || mode == 1, "group set_exchange: mode must be 0 (reduce kernel) or 1 (one-shot)");
+        if (mode == 1) {
+            std::vector<char*> inboxes;
+            for (auto& e : r) {
+                LLMI_TRY(e->alloc_xchg());
+                inboxes.push_back(e->inbox);
+            }
+            for (auto& e : r) LLMI_TRY(e->set_peers(inboxes));  // same device: the inboxes themselves
+        }
+        LLMI_HIP(hipStreamSynchronize(stream));
+        graphs.clear();
+        xchg_mode = mode;
+        return LLMI_OK;
+    }
+    // slot: 0 xacc, 1 res[0], 2 res[1], 3 argmax partials
+    int reduce(int slot, int n, int op) {
+        const int W = (int)r.size();
+        if (W == 1) return LLMI_OK;
+        if (xchg_mode == 0) return group_reduce_launch(ptrs + slot * W, W, n, op, stream);
+        auto buf = [&](Engine& e) -> void* {
+            return slot == 0 ? (void*)e.xacc : slot == 3 ? (void*)e.partials : (void*)e.res[slot - 1];
+        };
+        for (auto& e : r) LLMI_TRY(xchg_launch(e->xchg_args(buf(*e), n, op, 1), stream));
+        for (auto& e : r) LLMI_TRY(xchg_launch(e->xchg_args(buf(*e), n, op, 2), stream));
+        return LLMI_OK;
+    }
+
     int record_step(int nact) {
-        const int W = (int)r.size(), H = r[0]->c.hidden;
+        const int H = r[0]->c.hidden;
         for (auto& e : r) e->rec_nact = nact;
         for (auto& e : r) LLMI_TRY(e->rec_start());
         for (int l = 0; l < r[0]->c.layers; ++l) {
             for (auto& e : r) LLMI_TRY(e->rec_attn(l));
-            if (W > 1) LLMI_TRY(group_reduce_launch(ptrs, W, H, 0, stream));
+            LLMI_TRY(reduce(0, H, 0));
             for (auto& e : r) LLMI_TRY(e->rec_ffn(l));
-            if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + (1 + (l + 1) % 2) * W, W, H, 0, stream));
+            LLMI_TRY(reduce(1 + (l + 1) % 2, H, 0));
         }
         for (auto& e : r) LLMI_TRY(e->rec_head());
-        if (W > 1) LLMI_TRY(group_reduce_launch(ptrs + 3 * W, W, r[0]->lm_grid, 2, stream));
-        return LLMI_OK;
+        return reduce(3, r[0]->lm_grid, 2);
     }
 
     int decode(int n, int use_graph) {
@@ -1197,6 +1303,64 @@ int llmi_engine_bytes(llmi_engine* e, uint64_t* weight_bytes, uint64_t* kv_bytes
 
 llmi_stream_t llmi_engine_stream(llmi_engine* e) { return e ? (llmi_stream_t)e->e.stream : nullptr; }
 
+int llmi_engine_xchg_handle(llmi_engine* e, void* out64) {
+    LLMI_REQUIRE(e && out64, "xchg_handle: null argument");
+    Engine& g = e->e;
+    LLMI_REQUIRE(!g.grouped, "xchg_handle: not on a group rank");
+    LLMI_HIP(hipSetDevice(g.device));
+    LLMI_TRY(g.alloc_xchg());
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle must be 64 bytes");
+    hipIpcMemHandle_t h;
+    LLMI_HIP(hipIpcGetMemHandle(&h, g.inbox));
+    std::memcpy(out64, &h, sizeof(h));
+    return LLMI_OK;
+}
+
+int llmi_engine_xchg_open(llmi_engine* e, const void* handles) {
+    LLMI_REQUIRE(e && handles, "xchg_open: null argument");
+    Engine& g = e->e;
+    LLMI_REQUIRE(!g.grouped && g.inbox, "xchg_open: call llmi_engine_xchg_handle first");
+    LLMI_REQUIRE(!g.peers_ready, "xchg_open: already open");
+    LLMI_HIP(hipSetDevice(g.device));
+    const int W = g.c.tp_world;
+    std::vector<char*> p(W, nullptr);
+    for (int q = 0; q < W; ++q) {
+        if (q == g.c.tp_rank) {
+            p[q] = g.inbox;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, static_cast<const char*>(handles) + (size_t)q * 64, 64);
+        void* ptr = nullptr;
+        LLMI_HIP(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+        g.peers_opened.push_back(ptr);
+        p[q] = static_cast<char*>(ptr);
+    }
+    LLMI_TRY(g.set_peers(p));
+    g.peers_ready = true;
+    return LLMI_OK;
+}
+
+int llmi_engine_set_exchange(llmi_engine* e, int mode) {
+    LLMI_REQUIRE(e, "set_exchange: null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.set_exchange(mode);
+}
+
+int llmi_group_set_exchange(llmi_group* g, int mode) {
+    LLMI_REQUIRE(g, "group_set_exchange: null group");
+    return g->g.set_exchange(mode);
+}
+
+int llmi_engine_debug_set_next_pos(llmi_engine* e, int next_pos) {
+    LLMI_REQUIRE(e, "debug_set_next_pos: null engine");
+    Engine& g = e->e;
+    LLMI_HIP(hipSetDevice(g.device));
+    LLMI_HIP(hipStreamSynchronize(g.stream));
+    LLMI_HIP(hipMemcpy(&g.st->next_pos, &next_pos, sizeof(int), hipMemcpyHostToDevice));
+    return LLMI_OK;
+}
+
 int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf) {
     LLMI_REQUIRE(e, "debug_stamps: null engine");
     e->e.dbg_stamps = static_cast<unsigned long long*>(dev_buf);
@@ -1230,10 +1394,15 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
                 LLMI_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce(int64): ") + ncclGetErrorString(r));
                 return LLMI_OK;
             }
+            case 8:
+            case 9:  // the same exchange over the one-shot peer path
+                return llmi::xchg_launch(g.xchg_args(g.xacc, (int)H, 0, 3), g.stream);
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..7");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..9");
     };
-    LLMI_REQUIRE(which < 6 || g.comm != nullptr, "time_kernel: the all-reduce needs an RCCL communicator (tp_id)");
+    LLMI_REQUIRE(which < 6 || which > 7 || g.comm != nullptr,
+                 "time_kernel: the all-reduce needs an RCCL communicator (tp_id)");
+    LLMI_REQUIRE(which < 8 || g.peers_ready, "time_kernel: the one-shot exchange needs xchg_open");
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
         case 0: b = (uint64_t)(g.ql + 2 * g.kvrows) * H * ws + (g.ql + 2 * g.kvrows) * sc; break;
@@ -1249,7 +1418,9 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
         case 4: b = (uint64_t)H * g.il * ws + H * sc; break;
         case 5: b = (uint64_t)g.vl * H * g.esz; break;
         case 6:
-        case 7: b = (uint64_t)H * 8; break;
+        case 7:
+        case 8:
+        case 9: b = (uint64_t)H * 8; break;
     }
     // timing launches modify the residual stream (o/down epilogues add into x),
     // so save and restore the small activation state around them
@@ -1258,10 +1429,28 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     long long* fx[3] = {g.xacc, g.res[0], g.res[1]};
     for (int i = 0; i < 3; ++i)
         LLMI_HIP(hipMemcpyAsync(save_fx.data() + i * H * 8, fx[i], H * 8, hipMemcpyDeviceToHost, g.stream));
+    // the attention launches write the current position's K/V row into every layer they
+    // cycle through (from the last layer's q/k/v): keep each layer's row at cur_pos
+    llmi::DecodeState hst{};
+    std::vector<char> save_kv;
+    const size_t kv_eb = llmi::dtype_size(g.c.kv_dtype), kv_row = (size_t)g.c.head_dim * kv_eb;
+    const size_t kv_pitch = (size_t)g.c.max_seq * kv_row;
+    auto kv_rows = [&](int l, int v) {
+        return (char*)(v ? g.vcache : g.kcache) + (size_t)l * g.kv_layer_elems * kv_eb + (size_t)hst.cur_pos * kv_row;
+    };
+    if (which == 1) {
+        LLMI_HIP(hipMemcpyAsync(&hst, g.st, sizeof(hst), hipMemcpyDeviceToHost, g.stream));
+        LLMI_HIP(hipStreamSynchronize(g.stream));
+        save_kv.resize((size_t)g.c.layers * 2 * g.kvl * kv_row);
+        for (int l = 0; l < g.c.layers; ++l)
+            for (int v = 0; v < 2; ++v)
+                LLMI_HIP(hipMemcpy2D(save_kv.data() + ((size_t)l * 2 + v) * g.kvl * kv_row, kv_row, kv_rows(l, v),
+                                     kv_pitch, kv_row, g.kvl, hipMemcpyDeviceToHost));
+    }
     LLMI_TRY(launch());  // warm
     hipGraph_t cg = nullptr;
     hipGraphExec_t ce = nullptr;
-    if (which == 7) {  // the all-reduces captured into one graph, as the decode step replays them
+    if (which == 7 || which == 9) {  // the exchanges captured into one graph, as the decode step replays them
         LLMI_HIP(hipStreamBeginCapture(g.stream, hipStreamCaptureModeThreadLocal));
         for (int i = 0; i < iters; ++i) LLMI_TRY(launch());
         LLMI_HIP(hipStreamEndCapture(g.stream, &cg));
@@ -1287,6 +1476,11 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     if (cg) (void)hipGraphDestroy(cg);
     LLMI_HIP(hipMemcpy(g.x, save.data(), H * 4, hipMemcpyHostToDevice));
     for (int i = 0; i < 3; ++i) LLMI_HIP(hipMemcpy(fx[i], save_fx.data() + i * H * 8, H * 8, hipMemcpyHostToDevice));
+    if (which == 1)
+        for (int l = 0; l < g.c.layers; ++l)
+            for (int v = 0; v < 2; ++v)
+                LLMI_HIP(hipMemcpy2D(kv_rows(l, v), kv_pitch, save_kv.data() + ((size_t)l * 2 + v) * g.kvl * kv_row,
+                                     kv_row, kv_row, g.kvl, hipMemcpyHostToDevice));
     *avg_us = ms * 1000.f / iters;
     if (bytes) *bytes = b;
     return LLMI_OK;

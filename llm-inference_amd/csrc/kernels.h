@@ -168,6 +168,9 @@ struct AttnArgs {
     // K/V load is issued before the device position arrives; 0: grid = max_seq / 64,
     // inactive splits exit after reading the position
     int nact = 0;
+    // HOST_SIZED (nact > 0): the kernel checks nact against the device position; on a
+    // mismatch it sets bit 4 here (DecodeState::error) and does no work
+    int* err = nullptr;
 };
 
 // Merge of the split partials fused into the o_proj, split by head: workgroup
@@ -211,7 +214,8 @@ struct DecodeState {
     int cur_pos;      // position of the forward in flight
     int prompt_len;
     int vocab;
-    int error;        // sticky error flags (1: token id out of range, 2: position overflow)
+    int error;        // sticky error flags (1: token id out of range, 2: position overflow,
+                      // 4: host-sized attention grid != device position's split count)
     int pad[3];
 };
 
@@ -267,6 +271,23 @@ int sampling_launch(const int32_t* topk_ids, void* topk_vals, int dtype, int row
 int repeat_kv_launch(const void* k_cache, const void* v_cache, int dtype, int layer, const int* ctx_len, int batch,
                      int kv_heads, int max_seq, int heads, int max_k_len, int d, void* k_dst, void* v_dst,
                      hipStream_t s);
+
+// --------------------------------------------- one-shot TP exchange (xchg.hip)
+constexpr int kXchgSlice = 256;     // vector elements per workgroup
+constexpr int kXchgMaxSlices = 64;  // n <= 16384 elements
+struct XchgArgs {
+    long long* buf = nullptr;         // this rank's contribution in, the reduction out (n 8-B elements)
+    int n = 0;
+    int op = 0;                       // 0: int64 sum, 2: uint64 max
+    int rank = 0, world = 1;
+    char* const* peers = nullptr;     // device array [world]: every rank's inbox (peers[rank] = own)
+    unsigned long long* ep = nullptr; // [kXchgMaxSlices] epoch counters (this rank's memory)
+    int* err = nullptr;               // DecodeState::error; bit 8 = a peer never arrived (timeout)
+    int mode = 3;                     // 1: push only, 2: wait + reduce only, 3: both
+    int cap_n = 0, cap_w = 0;         // inbox geometry: elements per slot, slots per phase
+};
+size_t xchg_inbox_bytes(int world, int cap_n);
+int xchg_launch(const XchgArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------- synthetic
 // in-place reduction over W rank buffers (device array of pointers); op 0 i64 sum, 1 f32 sum, 2 u64 max

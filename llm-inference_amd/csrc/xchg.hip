@@ -1,0 +1,121 @@
+// One-shot peer-write exchange for tensor-parallel decode (config 4).
+//
+// What it replaces: the RCCL all-reduces of the decode step -- the int64 fixed-point
+// residual after o_proj and after down (2 per layer) and the uint64 max of the
+// vocab-parallel argmax keys (1 per token): the sum of the row-parallel partials of
+// modeling_llama.py's `pretraining_tp` (modeling_llama.py:251-266, 443-446). Each is a
+// 32 KB message, far too small to be bandwidth-bound on xGMI: RCCL's ring/tree steps
+// make it latency-bound (2 L + 1 = 65 of them per 7B token).
+//
+// One launch per exchange instead, no collective library:
+//   * every rank owns an INBOX in its own HBM (uncached, hipDeviceMallocUncached, so a
+//     peer's write over xGMI is what a later load returns): data [2 phases][world][cap_n]
+//     int64 and flags [2 phases][world][kXchgMaxSlices] uint64; every rank holds the
+//     IPC-mapped inbox base of every peer (peers[q]);
+//   * workgroup g owns slice g (kXchgSlice elements) of the vector: it writes its
+//     rank's slice into slot [phase][rank] of EVERY rank's inbox (its own too), then
+//     -- after a system-scope release -- stores the exchange's epoch into flag
+//     [phase][rank][g] of every inbox;
+//   * then it waits until flag [phase][q][g] of its own inbox holds the epoch for every
+//     rank q, and reduces the W slots in rank order (int64 sum: exact, so the result
+//     is bitwise the RCCL one and independent of arrival order; uint64 max) into buf.
+// Epochs: a per-slice counter in the rank's own memory (e = count + 1); phase = e & 1.
+// A rank can run at most one exchange ahead of the slowest peer (its next push needs
+// every peer's flag of the current one), so two phases never alias.
+// Liveness: every wait is bounded (kXchgTimeoutTicks of the 100 MHz clock); a timeout
+// sets bit 8 of the decode state's error word -- tokens_out raises -- and later waits
+// of the run are skipped, so a lost peer ends the run with an error instead of a hang.
+#include "kernels.h"
+
+namespace llmi {
+namespace {
+
+constexpr int kXThreads = kXchgSlice / 2;          // two 8-B elements (one 16-B access) per thread
+constexpr unsigned long long kXchgTimeoutTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ size_t data_elems(const XchgArgs& a) { return (size_t)2 * a.cap_w * a.cap_n; }
+
+__global__ __launch_bounds__(kXThreads) void xchg_kernel(XchgArgs a) {
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const int i0 = g * kXchgSlice + 2 * tid;
+    const unsigned long long e = a.ep[g] + 1;
+    const int ph = (int)(e & 1ull);
+    auto slot = [&](char* base, int q) {
+        return reinterpret_cast<long long*>(base) + ((size_t)ph * a.cap_w + q) * a.cap_n;
+    };
+    auto flag = [&](char* base, int q) {
+        return reinterpret_cast<unsigned long long*>(reinterpret_cast<long long*>(base) + data_elems(a)) +
+               ((size_t)ph * a.cap_w + q) * kXchgMaxSlices + g;
+    };
+    if (a.mode & 1) {  // push: this rank's slice into slot [ph][rank] of every inbox
+        longlong2 v = make_longlong2(0, 0);
+        if (i0 + 1 < a.n) {
+            v = *reinterpret_cast<const longlong2*>(a.buf + i0);
+        } else if (i0 < a.n) {
+            v.x = a.buf[i0];
+        }
+        if (i0 < a.n)
+            for (int q = 0; q < a.world; ++q) *reinterpret_cast<longlong2*>(slot(a.peers[q], a.rank) + i0) = v;
+        __threadfence_system();  // every lane's data is visible system-wide ...
+        __syncthreads();         // ... before lane 0 raises the flags
+        if (tid == 0)
+            for (int q = 0; q < a.world; ++q)
+                __hip_atomic_store(flag(a.peers[q], a.rank), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (a.mode & 2) {  // wait for every rank's slice, reduce in rank order
+        char* own = a.peers[a.rank];
+        if (tid < a.world) {
+            unsigned long long* f = flag(own, tid);
+            const bool dead = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8;
+            if (!dead) {
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                for (unsigned it = 0;; ++it) {
+                    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == e) break;
+                    if ((it & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
+                        atomicOr(a.err, 8);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+        }
+        __syncthreads();
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the slots written by the peers
+        if (i0 < a.n) {
+            long long s0 = 0, s1 = 0;
+            unsigned long long m0 = 0, m1 = 0;
+            for (int q = 0; q < a.world; ++q) {
+                const longlong2 v = *reinterpret_cast<const longlong2*>(slot(own, q) + i0);
+                s0 += v.x;
+                s1 += v.y;
+                m0 = max(m0, (unsigned long long)v.x);
+                m1 = max(m1, (unsigned long long)v.y);
+            }
+            a.buf[i0] = a.op == 0 ? s0 : (long long)m0;
+            if (i0 + 1 < a.n) a.buf[i0 + 1] = a.op == 0 ? s1 : (long long)m1;
+        }
+        if (tid == 0) a.ep[g] = e;
+    }
+}
+
+}  // namespace
+
+size_t xchg_inbox_bytes(int world, int cap_n) {
+    return (size_t)2 * world * cap_n * 8 + (size_t)2 * world * kXchgMaxSlices * 8;
+}
+
+int xchg_launch(const XchgArgs& a, hipStream_t s) {
+    LLMI_REQUIRE(a.buf && a.peers && a.ep && a.err, "xchg: null pointer");
+    LLMI_REQUIRE(a.world >= 1 && a.world <= a.cap_w && a.rank >= 0 && a.rank < a.world, "xchg: bad rank/world");
+    LLMI_REQUIRE(a.n >= 0 && a.n <= a.cap_n && a.n <= kXchgSlice * kXchgMaxSlices, "xchg: n exceeds the inbox");
+    LLMI_REQUIRE(a.cap_n % 2 == 0, "xchg: inbox slots must hold an even element count (16-B accesses)");
+    LLMI_REQUIRE(a.op == 0 || a.op == 2, "xchg: op must be 0 (int64 sum) or 2 (uint64 max)");
+    LLMI_REQUIRE(a.mode >= 1 && a.mode <= 3, "xchg: mode must be 1 (push), 2 (reduce) or 3 (both)");
+    if (a.n == 0) return LLMI_OK;
+    const int grid = (a.n + kXchgSlice - 1) / kXchgSlice;
+    hipLaunchKernelGGL(xchg_kernel, dim3(grid), dim3(kXThreads), 0, s, a);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+}  // namespace llmi

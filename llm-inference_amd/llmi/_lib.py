@@ -89,6 +89,11 @@ _SIGS = {
     "llmi_engine_stream": (_P, [_P]),
     "llmi_engine_time_kernel": (_I, [_P, _I, _I, C.POINTER(_F), C.POINTER(_U64)]),
     "llmi_engine_debug_stamps": (_I, [_P, _P]),
+    "llmi_engine_debug_set_next_pos": (_I, [_P, _I]),
+    "llmi_engine_xchg_handle": (_I, [_P, _P]),
+    "llmi_engine_xchg_open": (_I, [_P, _P]),
+    "llmi_engine_set_exchange": (_I, [_P, _I]),
+    "llmi_group_set_exchange": (_I, [_P, _I]),
     "llmi_group_create": (_I, [C.POINTER(Config), _I, _I, C.POINTER(_P)]),
     "llmi_group_destroy": (_I, [_P]),
     "llmi_group_load_synthetic": (_I, [_P, _U64]),

@@ -120,13 +120,34 @@ class Engine:
         call("llmi_engine_bytes", self._h, C.byref(w), C.byref(kv))
         return w.value, kv.value
 
+    def debug_set_next_pos(self, next_pos: int):
+        """Test hook: move the device decode state's next position only (not the host's)."""
+        call("llmi_engine_debug_set_next_pos", self._h, int(next_pos))
+
     def stream(self) -> int:
         return _lib.lib().llmi_engine_stream(self._h) or 0
 
     # allreduce / allreduce_graph: one residual all-reduce of the TP exchange (needs a tp_id),
     # launched eagerly / replayed from a captured graph of `iters` calls
     KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5, "allreduce": 6,
-               "allreduce_graph": 7}
+               "allreduce_graph": 7, "xchg": 8, "xchg_graph": 9}
+
+    # one-shot peer exchange (tensor parallel without RCCL in the token graph)
+    def xchg_handle(self) -> bytes:
+        buf = C.create_string_buffer(64)
+        call("llmi_engine_xchg_handle", self._h, buf)
+        return buf.raw
+
+    def xchg_open(self, handles):
+        """handles: every rank's 64-byte inbox handle, in rank order."""
+        blob = b"".join(bytes(h) for h in handles)
+        assert len(blob) == 64 * self.cfg.tp_world
+        buf = C.create_string_buffer(blob, len(blob))
+        call("llmi_engine_xchg_open", self._h, buf)
+
+    def set_exchange(self, mode: int):
+        """0: RCCL all-reduces (needs a tp_id at create); 1: the one-shot peer exchange."""
+        call("llmi_engine_set_exchange", self._h, int(mode))
 
     def time_kernel(self, which: str, iters: int = 50):
         us, b = C.c_float(), C.c_uint64()
@@ -198,6 +219,10 @@ class TPGroup:
         out = np.zeros(self.cfg.hidden, np.float32)
         call("llmi_group_hidden", self._h, rank, out.ctypes.data, self.cfg.hidden)
         return out
+
+    def set_exchange(self, mode: int):
+        """0: in-place reduction kernel; 1: the one-shot peer exchange kernels."""
+        call("llmi_group_set_exchange", self._h, int(mode))
 
     def generate(self, prompt, n_new: int, use_graph: bool = True) -> np.ndarray:
         prompt = np.ascontiguousarray(prompt, np.int32)

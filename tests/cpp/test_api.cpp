@@ -157,6 +157,47 @@ static void layer_decode(const std::vector<int>& prompt, int n_new, uint64_t see
     for (size_t i = 0; i < gen.size(); ++i) std::printf("%s%d", i ? ", " : "", gen[i]);
     std::printf("]}\n");
 
+    // ---- the same decode with the reference's fp16 activations (Llama<half>:
+    // TensorWrapper<half> decoder_input / decoder_output, self_decoder.cpp:59-81); the
+    // layers stage them through fp32, so the tokens must equal the fp32 run's
+    {
+        Dev<half_t> x16(H), y16(H);
+        Dev<float> kc16((size_t)L * kv * S * hd), vc16((size_t)L * kv * S * hd);
+        TensorWrapper<half_t> in16(GPU, FP16, {1, H}, x16.p), out16(GPU, FP16, {1, H}, y16.p);
+        TensorWrapper<float> kcache16(GPU, FP32, {L, 1, kv, S, hd}, kc16.p), vcache16(GPU, FP32, {L, 1, kv, S, hd}, vc16.p);
+        TensorMap hin{{"decoder_input", &in16}, {"step", &step_t}, {"finished", &fin_t}};
+        TensorMap hout{{"decoder_output", &out16}, {"all_k_cache", &kcache16}, {"all_v_cache", &vcache16}};
+        std::vector<int> gen16;
+        tok = prompt[0];
+        for (int pos = 0; pos < (int)prompt.size() + n_new - 1; ++pos) {
+            if (pos < (int)prompt.size()) tok = prompt[pos];
+            LLMI_CALL(llmi_memcpy(ids.p, &tok, 4, 0));
+            launchInputEmbedding(&id_t, &in16, &E);
+            step = pos + 1;
+            dec.forward(hin, lw, hout, dp);
+            LLMI_CALL(llmi_convert(y16.p, LLMI_F16, y.p, LLMI_F32, H, nullptr));  // head in fp32, as above
+            launchRMSNorm(&dec_out, &un, FN, 1e-5f, true);
+            launchLinearGemm(&dec_out, LM, &probs, nullptr, false, true);
+            launchTopKforBeamSearch(&probs, &next_t);
+            LLMI_CALL(llmi_memcpy(&tok, next.p, 4, 1));
+            if (pos >= (int)prompt.size() - 1) gen16.push_back(tok);
+        }
+        std::printf("{\"layer_api_tokens_half\": [");
+        for (size_t i = 0; i < gen16.size(); ++i) std::printf("%s%d", i ? ", " : "", gen16[i]);
+        std::printf("]}\n");
+        // an activation of another dtype is an error (the reference's as<T>() read it silently)
+        Dev<int> bad(H);
+        TensorWrapper<int> bad_t(GPU, INT32, {1, H}, bad.p);
+        TensorMap bin{{"decoder_input", &bad_t}, {"step", &step_t}, {"finished", &fin_t}};
+        bool threw = false;
+        try {
+            dec.forward(bin, lw, hout, dp);
+        } catch (const std::runtime_error&) {
+            threw = true;
+        }
+        report("layer_rejects_int32_activations", threw ? 0.0 : 1.0, 0.0);
+    }
+
     // ---- the same request with the prompt through LlamaContextDecoder in ONE batched
     // pass (context_decoder.cpp:47-143, the reference's firstTokenGen path), then the
     // self decoder from position n on (fresh fp32 caches)

@@ -27,7 +27,12 @@ static std::string json_escape(const std::string& s) {
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
     Tokenizer tok;
-    tok.Initialize(argv[1]);
+    try {
+        tok.Initialize(argv[1]);
+    } catch (const std::exception& e) {  // a malformed vocabulary file is reported, never parsed on
+        std::fprintf(stderr, "%s\n", e.what());
+        return 3;
+    }
     std::string line;
     while (std::getline(std::cin, line)) {
         std::vector<int> ids = tok.Encode(line);

@@ -184,3 +184,22 @@ def test_graph_per_split_count_across_chunk_boundaries():
     r = rel(outs[0][1], ologits)
     print(f"nact graphs, {n_new} tokens to ctx {len(f['prompt']) + n_new - 1}: logits rel-L2 {r:.2e}")
     assert r < LOGIT_TOL
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_host_device_position_mismatch_is_reported(use_graph):
+    """The attention / o_proj grids are sized from the host's position (one graph per split
+    count). If the device decode state disagrees, the attention kernel must flag it (error
+    bit 4) instead of dropping keys or merging stale partials -- tokens() raises."""
+    cfg = preset("tiny", max_seq=256)
+    cfg.kv_dtype = _lib.F32
+    f = load("tiny.npz")
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        e.set_prompt(f["prompt"])
+        e.decode(len(f["prompt"]), use_graph=use_graph)
+        e.tokens()  # consistent so far: no error
+        e.debug_set_next_pos(100)  # device at position 100 (2 splits), host still at 8 (1 split)
+        e.decode(1, use_graph=use_graph)
+        with pytest.raises(_lib.LlmiError, match="device error flag 4"):
+            e.tokens()

@@ -120,3 +120,28 @@ def test_f7_longctx_prefill_2040_then_decode_to_ctx_2048():
     np.testing.assert_array_equal(toks, f["tokens"])
     assert o.pos == 2048  # the last forward ran at position 2047
     assert rel_l2(logits, f["last_logits"]) < 1e-5
+
+
+@pytest.mark.parametrize("name,cfg", [
+    ("f8_ctx_history_tiny.npz", R.LlamaConfig(hidden=512, heads=4, kv_heads=4, inter=1024, layers=2, vocab=32000,
+                                              max_seq=64)),
+    ("f8_ctx_history_7b.npz", R.LlamaConfig(layers=2, max_seq=64)),
+])
+def test_f8_context_chunk_after_history(name, cfg):
+    """Pins the oracle's chunked prefill (a chunk starting at position h > 0 over a cache
+    holding h history positions) against the reference's per-sequence cached run
+    (f8: histories {0, 5, 17}, chunks {8, 4, 11}): history K/V, written K/V, logits."""
+    f = load(name)
+    for b, (h, q) in enumerate(zip(f["hist"], f["lens"])):
+        o = R.LlamaOracle(cfg, seed=int(f["seed"]))
+        ids = f[f"ids{b}"]
+        if h > 0:
+            o.prefill(ids[:h])
+            for l in range(cfg.layers):
+                assert rel_l2(o.k_cache[l, :, :h], f[f"hist_k{b}"][l]) < 1e-5
+                assert rel_l2(o.v_cache[l, :, :h], f[f"hist_v{b}"][l]) < 1e-5
+        logits = o.prefill(ids[h:])
+        assert rel_l2(logits, f[f"logits{b}"]) < 1e-5, b
+        nh = f[f"new_k{b}"].shape[0]
+        assert rel_l2(o.k_cache[cfg.layers - 1, :nh, h:h + q], f[f"new_k{b}"]) < 1e-5
+        assert rel_l2(o.v_cache[cfg.layers - 1, :nh, h:h + q], f[f"new_v{b}"]) < 1e-5

@@ -34,3 +34,35 @@ def test_tokenizer_under_asan_ubsan(tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stderr
     assert len(r.stdout.splitlines()) == 6 and "ERROR" not in r.stderr
+
+
+def _flm(*fields):
+    """A minimal .flm vocabulary file: version 0, then the given int32 / float32 fields."""
+    import struct
+    out = struct.pack("<i", 0)
+    for f in fields:
+        out += struct.pack("<f", f) if isinstance(f, float) else struct.pack("<i", f)
+    return out
+
+
+@pytest.mark.parametrize("name,data", [
+    ("truncated", None),                                   # the real file cut short
+    ("negative_id", _flm(1, 1, ord("a"), -5, 0.0)),
+    ("huge_count", _flm(0x7FFFFFFF)),
+    ("negative_len", _flm(1, -3)),
+    ("oversized_len", _flm(1, 1 << 20)),
+    ("id_too_large", _flm(1, 1, ord("a"), 1 << 30, 0.0)),
+])
+def test_tokenizer_rejects_malformed_files_under_asan(tmp_path, name, data):
+    """The vocabulary file is external data (Tokenizer::Initialize, tokenizer.h:137-167 in the
+    reference reads it unchecked): malformed counts, lengths and ids, and short reads, raise a
+    clean error without touching memory out of bounds."""
+    f = tmp_path / f"{name}.bin"
+    if data is None:
+        with open(os.path.join(REPO, "tests", "golden", "llama2-7b-tokenizer.bin"), "rb") as src:
+            data = src.read()[:100_000]
+    f.write_bytes(data)
+    r = subprocess.run([_build(tmp_path, "test_tokenizer"), str(f)], input="hello\n", capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "Tokenizer:" in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr
