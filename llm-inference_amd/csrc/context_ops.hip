@@ -24,14 +24,19 @@ template <typename T> __device__ __forceinline__ void stf(T* p, float v) { *p = 
 template <> __device__ __forceinline__ void stf<__half>(__half* p, float v) { *p = __float2half(v); }
 
 // BuildCausalMasksConsideringContextPastKV (build_causal_mask.cu:4-45): one workgroup
-// per sequence; 1 where q < q_len, k < k_len and k_len - q_len <= k <= q + (k_len - q_len).
+// per sequence; 1 where q < q_len, k < k_len and k <= q + (k_len - q_len). Defect not
+// carried over: the reference's :29 also requires k >= k_len - q_len, which hides every
+// history position from the chunk's queries (its comment means to hide padding, but the
+// repeated cache holds exactly context_length valid keys); with a history that diverges
+// from modeling_llama.py's cached forward (tests/golden/f8_*: 0.18 rel-L2). With no
+// history (k_len == q_len) both tests are the same.
 template <typename T>
 __global__ void causal_mask_kernel(T* mask, const int* q_lens, const int* k_lens, int max_q, int max_k) {
     const int qlen = q_lens[blockIdx.x], klen = k_lens[blockIdx.x];
     T* m = mask + (size_t)blockIdx.x * max_q * max_k;
     for (int o = threadIdx.x; o < max_q * max_k; o += blockDim.x) {
         const int q = o / max_k, k = o % max_k;
-        const bool one = q < qlen && k < klen && k <= q + (klen - qlen) && k >= klen - qlen;
+        const bool one = q < qlen && k < klen && k <= q + (klen - qlen);
         stf(m + o, one ? 1.f : 0.f);
     }
 }

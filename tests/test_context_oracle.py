@@ -25,10 +25,24 @@ def test_rope_angles_equal_model_oracle():
 def test_causal_mask_hand_worked():
     m = C.causal_mask([2, 3], [2, 5], 3, 5)
     want0 = [[1, 0, 0, 0, 0], [1, 1, 0, 0, 0], [0, 0, 0, 0, 0]]
-    # k_len 5, q_len 3: the reference's :29 admits only the current chunk (k >= 2)
-    want1 = [[0, 0, 1, 0, 0], [0, 0, 1, 1, 0], [0, 0, 1, 1, 1]]
+    # k_len 5, q_len 3 (2 history positions): every history key is visible, as in
+    # modeling_llama.py's cached forward (the reference's :29 would also require k >= 2)
+    want1 = [[1, 1, 1, 0, 0], [1, 1, 1, 1, 0], [1, 1, 1, 1, 1]]
     np.testing.assert_array_equal(m[0], want0)
     np.testing.assert_array_equal(m[1], want1)
+
+
+def test_causal_mask_equals_reference_formula_without_history():
+    """The reference's own :29 test (with its k >= klen - qlen term) on batches with no
+    history: identical to the restated mask (the term only differs when klen > qlen)."""
+    rng = np.random.default_rng(7)
+    for _ in range(20):
+        lens = rng.integers(1, 12, size=4)
+        mq = mk = int(lens.max())
+        q = np.arange(mq)[:, None]
+        k = np.arange(mk)[None, :]
+        ref = np.asarray([(q < l) & (k < l) & (k <= q) & (k >= 0) for l in lens], np.float32)
+        np.testing.assert_array_equal(C.causal_mask(lens, lens, mq, mk), ref)
 
 
 def test_masked_softmax_rows():
