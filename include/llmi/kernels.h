@@ -33,17 +33,27 @@ inline void* attn_workspace(int heads, int head_dim, int max_seq) {
 inline int tokens_of(const Tensor* t) { return t->shape.size() >= 2 ? t->size() / t->shape.back() : 1; }
 
 // fp32 view of an activation tensor: TensorWrapper<float> as is; TensorWrapper<half_t>
-// converted into a per-slot device scratch buffer (load = copy the values in) and
-// written back rounded to fp16 by back()
-inline float* f32_scratch(int slot, size_t n) {
-    thread_local void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
-    thread_local size_t cap[4] = {0, 0, 0, 0};
-    if (n * sizeof(float) > cap[slot]) {
-        if (buf[slot]) LLMI_CALL(llmi_device_free(buf[slot]));
-        LLMI_CALL(llmi_device_alloc(&buf[slot], n * sizeof(float)));
-        cap[slot] = n * sizeof(float);
+// converted into a device scratch buffer (load = copy the values in) and written back
+// rounded to fp16 by back(). The scratch is per (host thread, stream, slot): launchers
+// on different streams never share one, and a buffer that must grow is freed only
+// after the device has drained (earlier launches may still read it). The buffers live
+// for the thread (the reference's launchers allocate nothing; this is their staging).
+inline float* f32_scratch(int slot, size_t n, void* stream) {
+    struct Slots {
+        void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+        size_t cap[4] = {0, 0, 0, 0};
+    };
+    thread_local std::unordered_map<void*, Slots> per_stream;
+    Slots& s = per_stream[stream];
+    if (n * sizeof(float) > s.cap[slot]) {
+        if (s.buf[slot]) {
+            LLMI_CALL(llmi_device_sync());
+            LLMI_CALL(llmi_device_free(s.buf[slot]));
+        }
+        LLMI_CALL(llmi_device_alloc(&s.buf[slot], n * sizeof(float)));
+        s.cap[slot] = n * sizeof(float);
     }
-    return static_cast<float*>(buf[slot]);
+    return static_cast<float*>(s.buf[slot]);
 }
 template <typename AT> struct Act;
 template <> struct Act<float> {
@@ -56,7 +66,7 @@ template <> struct Act<half_t> {
     float* p = nullptr;
     Act(TensorWrapper<half_t>* t_, int slot, void* stream, bool load) : t(t_) {
         if (!t) return;
-        p = f32_scratch(slot, t->size());
+        p = f32_scratch(slot, t->size(), stream);
         if (load) LLMI_CALL(llmi_convert(t->data, LLMI_F16, p, LLMI_F32, t->size(), stream));
     }
     void back(void* stream) {

@@ -86,12 +86,6 @@ __device__ __forceinline__ void rope_cs(int pos, int i, int d, float base, float
     *s = (float)sd;
 }
 
-#ifndef LLMI_OPROJ_NOMERGE
-#define LLMI_OPROJ_NOMERGE 0
-#endif
-#ifndef LLMI_OPROJ_NOATOMIC
-#define LLMI_OPROJ_NOATOMIC 0
-#endif
 constexpr int kCntWordsPerHead = 64;  // 256 B: heads' counters never share a line
 struct Ws {
     unsigned* counters;  // [heads][kCntWordsPerHead]: fused attention + o_proj arrivals (word 0) and
@@ -431,13 +425,6 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
     // registers before anything waits (a load stored straight to LDS makes the compiler
     // wait for it -- and for every load issued before it -- right there, which had
     // serialised the partials' latency in front of the W_o stream)
-#if LLMI_OPROJ_NOMERGE  // diagnostic only (wrong output): no partial loads, no merge
-    if (true) {
-        load_w();
-        if (tid < D) o_s[tid] = 1.0f;
-        __syncthreads();
-    } else
-#endif
     {
 #pragma unroll
     for (int i = 0; i < kMergeChunk; ++i) {
@@ -534,11 +521,7 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
         if (row < a.n_rows) {
             float v = y_s[tid];
             if (a.scales) v *= __half2float(a.scales[row]);
-#if LLMI_OPROJ_NOATOMIC  // diagnostic only (wrong sums): plain store instead of the atomic add
-            a.xacc[row] = to_fixed(v);
-#else
             atomicAdd(reinterpret_cast<unsigned long long*>(a.xacc + row), (unsigned long long)to_fixed(v));
-#endif
         }
     }
 }

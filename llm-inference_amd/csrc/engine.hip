@@ -49,16 +49,6 @@ namespace {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace
 
-// GEMV grid overrides for A/B builds (0 = gemv_grid's automatic choice)
-#ifndef LLMI_QKV_GRID
-#define LLMI_QKV_GRID 0
-#endif
-#ifndef LLMI_GU_GRID
-#define LLMI_GU_GRID 0
-#endif
-#ifndef LLMI_DOWN_GRID
-#define LLMI_DOWN_GRID 0
-#endif
 #ifndef LLMI_I8_DOWN_KSPLIT
 #define LLMI_I8_DOWN_KSPLIT 4  // int8 down K slices: 13B down 18.2 -> 16.5 us, 8-layer loop 682 -> 665 us (A/B)
 #endif
@@ -564,7 +554,6 @@ struct Engine {
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
-        a.grid = LLMI_QKV_GRID;
         return a;
     }
     AttnArgs attn_args(int l) const {
@@ -614,7 +603,6 @@ struct Engine {
         a.seed_keep = c.tp_rank == 0 ? 1 : 0;
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
-        a.grid = LLMI_GU_GRID;
         return a;
     }
     GemvArgs down_args(int l) const {
@@ -627,7 +615,6 @@ struct Engine {
         // int8 rows are half the bytes of fp16 ones: K slices keep the loads per row in
         // flight and the x image per workgroup small (exact: int64 atomics)
         a.ksplit = (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT : 1;
-        a.grid = LLMI_DOWN_GRID;
         return a;
     }
 

@@ -20,9 +20,6 @@ constexpr int kWavesPerBlock = kThreads / kWave;
 #ifndef LLMI_GEMV_PIPE16
 #define LLMI_GEMV_PIPE16 0  // bit EPI: software-pipelined fp16 stream for that epilogue
 #endif
-#ifndef LLMI_GEMV_FARPAIR
-#define LLMI_GEMV_FARPAIR 0  // bit EPI: a wave's ROWS rows are g + r * n_groups (far apart) instead of adjacent
-#endif
 constexpr int kUnrollMax = LLMI_GEMV_UNROLL;  // 16-B loads per row in flight per lane
 constexpr int kRows = LLMI_GEMV_ROWS;      // rows per wave (EPI_SILU_MUL always pairs 2)
 
@@ -120,10 +117,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
 
     auto rows_of = [&](int g, int* rows) {
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r)
-            rows[r] = (EPI == EPI_SILU_MUL)            ? g + r * a.pair_off
-                      : ((LLMI_GEMV_FARPAIR >> EPI) & 1) ? g + r * n_groups
-                                                         : g * ROWS + r;
+        for (int r = 0; r < ROWS; ++r) rows[r] = (EPI == EPI_SILU_MUL) ? g + r * a.pair_off : g * ROWS + r;
     };
     // Branch-free streaming: every lane always issues its ROWS x kUnroll loads; out of
     // range chunks/rows are clamped to a valid address and zeroed by a mask. A

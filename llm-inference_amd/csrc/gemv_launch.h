@@ -97,12 +97,6 @@ int pick_unroll(const GemvArgs& a, int groups) {
     int best = (EPI != EPI_ARGMAX && groups >= 4096 && groups <= 12288 && kUnrollMax >= 4) ? 4 : kUnrollMax;
     for (int u : {4, 5, 8})
         if (u <= kUnrollMax && slots(u) < slots(best)) best = u;
-#ifdef LLMI_GEMV_U_ATOMIC
-    if (EPI == EPI_ATOMIC && sizeof(WT) == 2) best = LLMI_GEMV_U_ATOMIC;
-#endif
-#ifdef LLMI_GEMV_U_STORE
-    if (EPI == EPI_STORE && sizeof(WT) == 2) best = LLMI_GEMV_U_STORE;
-#endif
     return best;
 }
 

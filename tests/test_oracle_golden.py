@@ -145,3 +145,16 @@ def test_f8_context_chunk_after_history(name, cfg):
         nh = f[f"new_k{b}"].shape[0]
         assert rel_l2(o.k_cache[cfg.layers - 1, :nh, h:h + q], f[f"new_k{b}"]) < 1e-5
         assert rel_l2(o.v_cache[cfg.layers - 1, :nh, h:h + q], f[f"new_v{b}"]) < 1e-5
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not os.path.exists("/root/reference/modeling_llama.py"), reason="the reference is not present")
+def test_golden_fixtures_reproduce_from_the_reference():
+    """gen_golden.py --check: every committed fixture regenerates from the reference's
+    modeling_llama.py (the oracle-emulation arrays of F7 within 1e-5, everything the
+    reference itself produces bit for bit)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(G, "gen_golden.py"), "--check"], capture_output=True, text=True,
+                       timeout=1500)
+    assert r.returncode == 0 and "fixtures reproduce" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
