@@ -32,6 +32,8 @@ def main():
     rank, world, device, n_new = int(rank), int(world), int(device), int(n_new)
     f = np.load(fixture, allow_pickle=False)
     cfg = preset(pname, tp_rank=rank, tp_world=world)
+    if os.environ.get("XCHG_LAYERS"):  # timing runs: a thin model of the preset's width
+        cfg.layers, cfg.max_seq = int(os.environ["XCHG_LAYERS"]), 64
     cfg.kv_dtype = _lib.F32
     with Engine(cfg, device=device) as e:  # no RCCL id: the one-shot exchange only
         e.load_synthetic(int(f["seed"]))
@@ -48,7 +50,11 @@ def main():
         for g in (True, False):
             toks[g] = e.generate(f["prompt"], n_new, use_graph=g)
         logits = e.logits()
-        np.savez(os.path.join(rdv, f"out_{rank}.npz"), tokens=toks[True], tokens_eager=toks[False], logits=logits)
+        timing = {}
+        if os.environ.get("XCHG_TIME"):  # a collective: every rank times the same calls
+            timing = {k: e.time_kernel(k, 256)[0] for k in ("xchg", "xchg_graph")}
+        np.savez(os.path.join(rdv, f"out_{rank}.npz"), tokens=toks[True], tokens_eager=toks[False], logits=logits,
+                 **{f"us_{k}": np.float64(v) for k, v in timing.items()})
         # stay alive until every rank is done (no inbox freed while a peer may still write it)
         open(os.path.join(rdv, f"done{rank}"), "w").close()
         wait_for([os.path.join(rdv, f"done{q}") for q in range(world)])

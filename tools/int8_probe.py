@@ -22,13 +22,15 @@ def main():
     with Engine(cfg) as e:
         e.load_synthetic(0)
         p = synth_prompt(0, 8, cfg.vocab)
-        e.generate(p, 64)
-        e.set_prompt(p)
-        e.sync()
-        t0 = time.perf_counter()
-        e.decode(256)
-        e.sync()
-        out["loop_us_per_token"] = round((time.perf_counter() - t0) / 256 * 1e6, 1)
+        eager = len(sys.argv) > 3 and sys.argv[3] == "eager"  # rocprofv3 cannot trace graph replays
+        e.generate(p, 64, use_graph=not eager)
+        if not eager:
+            e.set_prompt(p)
+            e.sync()
+            t0 = time.perf_counter()
+            e.decode(256)
+            e.sync()
+            out["loop_us_per_token"] = round((time.perf_counter() - t0) / 256 * 1e6, 1)
         for k in ("qkv", "attn", "o", "gate_up", "down", "lm_head"):
             us, b = e.time_kernel(k, 64)
             out[k] = {"us": round(us, 2), "GBps": round(b / us / 1e3, 1)}
