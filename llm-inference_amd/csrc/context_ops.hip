@@ -298,13 +298,104 @@ __global__ __launch_bounds__(256) void bmm_kernel(const T* A, const T* B, T* C, 
     }
 }
 
+// The same product on the matrix cores (v_mfma_f32_16x16x32_f16): 64 x 64 output tile
+// per 256-thread workgroup, 4 waves in 2 x 2, each 32 x 32 = 2 x 2 MFMA tiles, K in
+// 32-deep LDS slabs stored [row][k] for both operands (B as [n][k], whatever its memory
+// layout). fp16 storage enters the MFMA exactly (P = 1). fp32 storage is split while it
+// is staged, v = hi + lo (hi = fp16(v), lo = fp16(v - hi)), on BOTH operands, and the
+// three products hi.hi + hi.lo + lo.hi are accumulated in fp32 (the lo.lo term is below
+// 2^-22 relative): fp32-faithful like gemm.hip's activation split.
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+constexpr int kMT = 64, kMK = 32, kMLd = kMK + 8;  // tile, K slab, padded LDS row (halves)
+template <typename T, bool TA, bool TB>
+__global__ __launch_bounds__(256) void bmm_mfma_kernel(const T* A, const T* B, T* C, int m, int n, int k) {
+    constexpr int P = std::is_same<T, float>::value ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) _Float16 As[P][kMT * kMLd];
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[P][kMT * kMLd];
+    const size_t z = blockIdx.z;
+    A += z * m * (size_t)k;
+    B += z * k * (size_t)n;
+    C += z * m * (size_t)n;
+    const int r0 = blockIdx.y * kMT, c0 = blockIdx.x * kMT;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+    // staging: 8 elements per thread per operand; along k when k is the contiguous memory
+    // dimension, else along the row (coalesced either way)
+    auto stage = [&](const T* src, bool rows_contig, int rbase, int rlim, int ld_r, int ld_k, _Float16 (*dst)[kMT * kMLd],
+                     int k0) {
+        int rr, kk, dr, dk;
+        if (!rows_contig) { rr = t >> 2; kk = (t & 3) * 8; dr = 0; dk = 1; }
+        else              { kk = t >> 3; rr = (t & 7) * 8; dr = 1; dk = 0; }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int r = rr + e * dr, kx = kk + e * dk;
+            const int gr = rbase + r, gk = k0 + kx;
+            const float v = (gr < rlim && gk < k) ? ldf(src + (size_t)gr * ld_r + (size_t)gk * ld_k) : 0.f;
+            const _Float16 hi = (_Float16)v;
+            dst[0][r * kMLd + kx] = hi;
+            if constexpr (P == 2) dst[1][r * kMLd + kx] = (_Float16)(v - (float)hi);
+        }
+    };
+    f4_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    for (int k0 = 0; k0 < k; k0 += kMK) {
+        // A element (r, kx): TA ? A[kx * m + r] : A[r * k + kx]; B element (c, kx): TB ? B[c * k + kx] : B[kx * n + c]
+        stage(A, TA, r0, m, TA ? 1 : k, TA ? m : 1, As, k0);
+        stage(B, !TB, c0, n, TB ? k : 1, TB ? 1 : n, Bs, k0);
+        __syncthreads();
+        h8_t a[P][2], b[P][2];
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                a[p][i] = *reinterpret_cast<const h8_t*>(&As[p][(wr * 32 + i * 16 + fr) * kMLd + fk]);
+                b[p][i] = *reinterpret_cast<const h8_t*>(&Bs[p][(wc * 32 + i * 16 + fr) * kMLd + fk]);
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+                if constexpr (P == 2) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+                }
+            }
+        __syncthreads();
+    }
+    // C fragment (i, j) register q: row 16 i + 4 (lane >> 4) + q, column 16 j + (lane & 15)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + wr * 32 + 16 * i + 4 * (lane >> 4) + q, c = c0 + wc * 32 + 16 * j + fr;
+                if (r < m && c < n) stf(C + (size_t)r * n + c, acc[i][j][q]);
+            }
+}
+
 template <typename T>
 void bmm_dispatch(const void* a, const void* b, void* c, int batch, int m, int n, int k, bool ta, bool tb,
                   hipStream_t s) {
-    const dim3 grid((n + kBT - 1) / kBT, (m + kBT - 1) / kBT, batch);
     const T* A = (const T*)a;
     const T* B = (const T*)b;
     T* C = (T*)c;
+#ifndef LLMI_BMM_FMA_ONLY  // (A/B builds only: the sequential-FMA kernel for every shape)
+    if (m >= 16 && n >= 16 && k >= 16) {  // matrix cores (one 64 x 64 tile per workgroup)
+        const dim3 g((n + kMT - 1) / kMT, (m + kMT - 1) / kMT, batch);
+        if (!ta && !tb) hipLaunchKernelGGL((bmm_mfma_kernel<T, false, false>), g, dim3(256), 0, s, A, B, C, m, n, k);
+        if (!ta && tb) hipLaunchKernelGGL((bmm_mfma_kernel<T, false, true>), g, dim3(256), 0, s, A, B, C, m, n, k);
+        if (ta && !tb) hipLaunchKernelGGL((bmm_mfma_kernel<T, true, false>), g, dim3(256), 0, s, A, B, C, m, n, k);
+        if (ta && tb) hipLaunchKernelGGL((bmm_mfma_kernel<T, true, true>), g, dim3(256), 0, s, A, B, C, m, n, k);
+        return;
+    }
+#endif
+    const dim3 grid((n + kBT - 1) / kBT, (m + kBT - 1) / kBT, batch);
     if (!ta && !tb) hipLaunchKernelGGL((bmm_kernel<T, false, false>), grid, dim3(256), 0, s, A, B, C, m, n, k);
     if (!ta && tb) hipLaunchKernelGGL((bmm_kernel<T, false, true>), grid, dim3(256), 0, s, A, B, C, m, n, k);
     if (ta && !tb) hipLaunchKernelGGL((bmm_kernel<T, true, false>), grid, dim3(256), 0, s, A, B, C, m, n, k);

@@ -183,6 +183,35 @@ def test_strided_batch_gemm(ops, ta, tb, dt):
     assert rel(got, want) < (1e-6 if dt == torch.float32 else 1e-3)
 
 
+@pytest.mark.parametrize("shape,tb", [((512, 512, 128), True), ((512, 128, 512), False)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_strided_batch_gemm_attention_shapes_on_mfma(ops, shape, tb, dt):
+    """The context layer's QK^T ([heads, q, d] x [heads, k, d]^T) and PV ([heads, q, k] x
+    [heads, k, d]) at a 512-token 7B-width shape: the MFMA path (fp32 split into hi/lo fp16
+    planes on both operands, three products) against float64, and its time vs the
+    sequential-FMA reference kernel's size-independent bar."""
+    import time
+    rng = np.random.default_rng(9)
+    m, n, k = shape
+    a = rng.standard_normal((1, 32, m, k)).astype(np.float32)
+    b = rng.standard_normal((1, 32, n, k) if tb else (1, 32, k, n)).astype(np.float32)
+    if dt == torch.float16:
+        a, b = a.astype(np.float16).astype(np.float32), b.astype(np.float16).astype(np.float32)
+    ta_, tb_ = T(a, dt), T(b, dt)
+    got = N(ops.launchLinearStridedBatchGemm(ta_, tb_, trans_b=tb))
+    ob = np.swapaxes(b, -1, -2) if tb else b
+    want = np.matmul(a.astype(np.float64), ob.astype(np.float64))
+    r = rel(got, want)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        ops.launchLinearStridedBatchGemm(ta_, tb_, trans_b=tb)
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / 20 * 1e6
+    print(f"bmm {shape} tb={tb} {dt}: rel-L2 {r:.2e}, {us:.1f} us ({2 * 32 * m * n * k / us / 1e6:.1f} TFLOP/s)")
+    assert r < (1e-6 if dt == torch.float32 else 1e-3)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.int32, torch.int64])
 def test_tp_allreduce_single_rank(ops, dt):
     """llmi_tp_comm_create / llmi_tp_allreduce / llmi_tp_comm_destroy over RCCL with one
