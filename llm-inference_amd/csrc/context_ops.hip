@@ -244,10 +244,9 @@ namespace {
 // launchLinearStridedBatchGemm (linear.cu:126-229: cublas stridedBatchedGemm for QK^T
 // and PV of the unfused context attention): C[z] = op(A[z]) . op(B[z]), row-major,
 // A [m, k] (or [k, m] when trans_a), B [k, n] (or [n, k] when trans_b), fp32
-// accumulate. 64 x 64 output tile per 256-thread workgroup, 4 x 4 per thread, K in
-// 16-deep LDS slabs (padded rows: conflict-free). The engine's prefill does these
-// products on the matrix cores inside its fused attention (prefill.hip); this is the
-// operator-level form for callers of the unfused layer.
+// accumulate. This FMA kernel (64 x 64 output tile per 256-thread workgroup, 4 x 4 per
+// thread, K in 16-deep LDS slabs) serves shapes with m, n or k below one MFMA tile;
+// everything else goes to bmm_mfma_kernel below.
 constexpr int kBT = 64, kKT = 16;
 template <typename T, bool TA, bool TB>
 __global__ __launch_bounds__(256) void bmm_kernel(const T* A, const T* B, T* C, int m, int n, int k) {
@@ -319,21 +318,46 @@ __global__ __launch_bounds__(256) void bmm_mfma_kernel(const T* A, const T* B, T
     C += z * m * (size_t)n;
     const int r0 = blockIdx.y * kMT, c0 = blockIdx.x * kMT;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-    // staging: 8 elements per thread per operand; along k when k is the contiguous memory
-    // dimension, else along the row (coalesced either way)
+    // staging: 8 consecutive elements of the contiguous memory dimension per thread per
+    // operand -- along k when k is contiguous (one 16-B LDS store), else along the rows
+    // (8 scattered 2-B LDS stores); 16-B global loads where aligned and in bounds
     auto stage = [&](const T* src, bool rows_contig, int rbase, int rlim, int ld_r, int ld_k, _Float16 (*dst)[kMT * kMLd],
                      int k0) {
-        int rr, kk, dr, dk;
-        if (!rows_contig) { rr = t >> 2; kk = (t & 3) * 8; dr = 0; dk = 1; }
-        else              { kk = t >> 3; rr = (t & 7) * 8; dr = 1; dk = 0; }
+        const int rr = rows_contig ? (t & 7) * 8 : t >> 2, kk = rows_contig ? t >> 3 : (t & 3) * 8;
+        const int gr = rbase + rr, gk = k0 + kk;
+        const T* p0 = src + (size_t)gr * ld_r + (size_t)gk * ld_k;
+        const int lim = rows_contig ? rlim - gr : k - gk;              // elements left along the run
+        const bool ok_other = rows_contig ? gk < k : gr < rlim;        // the fixed coordinate in range
+        float v[8];
+        if (ok_other && lim >= 8 && (reinterpret_cast<uintptr_t>(p0) & 15) == 0) {
+            if constexpr (sizeof(T) == 2) {
+                const h8_t h = *reinterpret_cast<const h8_t*>(p0);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (float)h[e];
+            } else {
+                const f4_t x0 = *reinterpret_cast<const f4_t*>(p0), x1 = *reinterpret_cast<const f4_t*>(p0 + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { v[e] = x0[e]; v[4 + e] = x1[e]; }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (ok_other && e < lim) ? ldf(p0 + e) : 0.f;  // stride 1 along the run
+        }
+        h8_t hi, lo;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const int r = rr + e * dr, kx = kk + e * dk;
-            const int gr = rbase + r, gk = k0 + kx;
-            const float v = (gr < rlim && gk < k) ? ldf(src + (size_t)gr * ld_r + (size_t)gk * ld_k) : 0.f;
-            const _Float16 hi = (_Float16)v;
-            dst[0][r * kMLd + kx] = hi;
-            if constexpr (P == 2) dst[1][r * kMLd + kx] = (_Float16)(v - (float)hi);
+            hi[e] = (_Float16)v[e];
+            lo[e] = (_Float16)(v[e] - (float)hi[e]);
+        }
+        if (!rows_contig) {
+            *reinterpret_cast<h8_t*>(&dst[0][rr * kMLd + kk]) = hi;
+            if constexpr (P == 2) *reinterpret_cast<h8_t*>(&dst[1][rr * kMLd + kk]) = lo;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                dst[0][(rr + e) * kMLd + kk] = hi[e];
+                if constexpr (P == 2) dst[1][(rr + e) * kMLd + kk] = lo[e];
+            }
         }
     };
     f4_t acc[2][2];
@@ -385,7 +409,6 @@ void bmm_dispatch(const void* a, const void* b, void* c, int batch, int m, int n
     const T* A = (const T*)a;
     const T* B = (const T*)b;
     T* C = (T*)c;
-#ifndef LLMI_BMM_FMA_ONLY  // (A/B builds only: the sequential-FMA kernel for every shape)
     if (m >= 16 && n >= 16 && k >= 16) {  // matrix cores (one 64 x 64 tile per workgroup)
         const dim3 g((n + kMT - 1) / kMT, (m + kMT - 1) / kMT, batch);
         if (!ta && !tb) hipLaunchKernelGGL((bmm_mfma_kernel<T, false, false>), g, dim3(256), 0, s, A, B, C, m, n, k);
@@ -394,7 +417,6 @@ void bmm_dispatch(const void* a, const void* b, void* c, int batch, int m, int n
         if (ta && tb) hipLaunchKernelGGL((bmm_mfma_kernel<T, true, true>), g, dim3(256), 0, s, A, B, C, m, n, k);
         return;
     }
-#endif
     const dim3 grid((n + kBT - 1) / kBT, (m + kBT - 1) / kBT, batch);
     if (!ta && !tb) hipLaunchKernelGGL((bmm_kernel<T, false, false>), grid, dim3(256), 0, s, A, B, C, m, n, k);
     if (!ta && tb) hipLaunchKernelGGL((bmm_kernel<T, false, true>), grid, dim3(256), 0, s, A, B, C, m, n, k);
