@@ -61,6 +61,9 @@ int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales
     a.n_rows = n;
     a.k = k;
     a.epi = EPI_STORE;
+    if (w_dtype == LLMI_F16 && linear_mfma_supported(m, n, k) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(y) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0)
+        return linear_mfma_launch(x, w, y, m, n, k, STREAM(stream));  // context rows: the prefill's GEMMs
     if (m > 8 && gemm_supported(w_dtype, n, k, EPI_STORE) && (k % 4) == 0 &&
         (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0) {
         GemmArgs g;  // prefill: MFMA GEMM, fp32-faithful (split activations)

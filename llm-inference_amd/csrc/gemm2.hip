@@ -26,6 +26,9 @@
 // (P = 2 issues 2x that on the matrix cores).
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+#include <utility>
 
 #include "kernels.h"
 
@@ -402,6 +405,103 @@ int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_
 #undef RS_KS
 #undef RS_LAUNCH
     LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+// ------------------------------------------------ llmi_linear on the prefill GEMMs
+// The layer API's projections (launchLinearGemm, linear.cu:38-104: cublasGemmEx over
+// [num_tokens, k] x [n, k]^T) for fp16 weights: the fp32 input split into hi/lo planes
+// (fp32-faithful, as the engine's prefill), then the 256 x 256 ping-pong GEMM (gemm3)
+// when the rows fill its tiles, else gemm2; split-K slices when the tiles alone would
+// leave CUs idle, summed in slice order by slab_sum_kernel (deterministic). Workspace:
+// one growing device buffer per stream (a grow waits for the stream first).
+namespace {
+__global__ __launch_bounds__(kThreads) void planes_kernel(const float4* x, _Float16* hi, _Float16* lo, size_t n4) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < n4; i += (size_t)gridDim.x * kThreads) {
+        const float4 v = x[i];
+        const float e[4] = {v.x, v.y, v.z, v.w};
+        h4 h, l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            h[q] = (_Float16)e[q];
+            l[q] = (_Float16)(e[q] - (float)h[q]);
+        }
+        reinterpret_cast<h4*>(hi)[i] = h;
+        reinterpret_cast<h4*>(lo)[i] = l;
+    }
+}
+__global__ __launch_bounds__(kThreads) void slab_sum_kernel(const float4* slab, float4* y, int ks, size_t n4) {
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < n4; i += (size_t)gridDim.x * kThreads) {
+        float4 a = slab[i];
+        for (int s = 1; s < ks; ++s) {
+            const float4 b = slab[(size_t)s * n4 + i];
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        y[i] = a;
+    }
+}
+std::mutex g_ws_mu;
+std::unordered_map<hipStream_t, std::pair<void*, size_t>> g_ws;
+int linear_workspace(hipStream_t s, size_t bytes, char** out) {
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    auto& e = g_ws[s];
+    if (bytes > e.second) {
+        if (e.first) {  // earlier launches on this stream may still read it
+            LLMI_HIP(hipStreamSynchronize(s));
+            LLMI_HIP(hipFree(e.first));
+            e = {nullptr, 0};
+        }
+        LLMI_HIP(hipMalloc(&e.first, bytes));
+        e.second = bytes;
+    }
+    *out = static_cast<char*>(e.first);
+    return LLMI_OK;
+}
+int grid_of(size_t n4) { return (int)std::min<size_t>((n4 + kThreads - 1) / kThreads, 4096); }
+}  // namespace
+
+bool linear_mfma_supported(int m, int n, int k) {
+    return m >= 16 && k % 64 == 0 && gemm2_supported(n, k, EPI_STORE);
+}
+
+int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s) {
+    LLMI_REQUIRE(x && w && y && linear_mfma_supported(m, n, k), "linear_mfma: N a multiple of 128, K of 64, M >= 16");
+    LLMI_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
+                 "linear_mfma: x and y must be 16-B aligned");
+    const bool g3 = m >= 256 && gemm3_supported(n, k, EPI_STORE, 1);
+    const int tiles = g3 ? ((m + 255) / 256) * (n / 256) : ((m + 127) / 128) * (n / kBN);
+    int ks = 1;  // K slices while the tiles leave more than a third of the 256 CUs idle
+    while (tiles * ks < 160 && ks < 8) {
+        const int nk = ks * 2;
+        if (g3 ? !gemm3_supported(n, k, EPI_SLAB, nk) : k % (nk * kBK) != 0) break;
+        ks = nk;
+    }
+    const size_t plane = ((size_t)m * k * 2 + 255) / 256 * 256;
+    const size_t slab = ks > 1 ? (size_t)ks * m * n * 4 : 0;
+    char* ws = nullptr;
+    LLMI_TRY(linear_workspace(s, 2 * plane + slab, &ws));
+    _Float16* hi = reinterpret_cast<_Float16*>(ws);
+    _Float16* lo = reinterpret_cast<_Float16*>(ws + plane);
+    const size_t n4x = (size_t)m * k / 4;
+    hipLaunchKernelGGL(planes_kernel, dim3(grid_of(n4x)), dim3(kThreads), 0, s, reinterpret_cast<const float4*>(x), hi,
+                       lo, n4x);
+    LLMI_HIP(hipGetLastError());
+    Gemm2Args g;
+    g.a[0] = hi; g.a[1] = lo; g.planes = 2; g.lda = k;
+    g.w = w; g.m = m; g.n = n; g.k = k; g.ldy = n;
+    if (ks > 1) {
+        g.epi = EPI_SLAB; g.ksplit = ks; g.slab = reinterpret_cast<float*>(ws + 2 * plane); g.y = y;
+    } else {
+        g.epi = EPI_STORE; g.y = y;
+    }
+    LLMI_TRY(g3 ? gemm3_launch(g, s) : gemm2_launch(g, s));
+    if (ks > 1) {
+        const size_t n4y = (size_t)m * n / 4;
+        hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_of(n4y)), dim3(kThreads), 0, s,
+                           reinterpret_cast<const float4*>(g.slab), reinterpret_cast<float4*>(y), ks, n4y);
+        LLMI_HIP(hipGetLastError());
+    }
     return LLMI_OK;
 }
 

@@ -102,6 +102,10 @@ int gemm2_launch(Gemm2Args a, hipStream_t s);
 // the same GEMM on 256 x 256 tiles with a ping-pong 8-wave schedule (gemm3.hip)
 bool gemm3_supported(int n, int k, int epi, int ksplit);
 int gemm3_launch(Gemm2Args a, hipStream_t s);
+// llmi_linear for fp16 weights (the layer API's projections): fp32 x split into planes,
+// then gemm3 / gemm2 (+ split-K slices summed in order); see gemm2.hip
+bool linear_mfma_supported(int m, int n, int k);
+int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s);
 // rows of x (+= the ksplit slices of slab, in slice order, written back to x),
 // then optional RMSNorm, then fp16 planes hi[, lo] (hi null: the combine alone)
 int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,
