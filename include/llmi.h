@@ -341,6 +341,14 @@ int llmi_engine_set_exchange(llmi_engine* e, int mode);
  * workgroup at 8 * linear block id: start, two kernel-defined marks, end, CU id;
  * 100 MHz clock). NULL switches it off. */
 int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf);
+/* Graph-replay timeline: like llmi_engine_debug_stamps, but every stamped launch of a
+ * recorded token step (qkv, attention, o_proj, gate_up, down per layer, then lm_head)
+ * writes its own region of slot_wgs workgroups x 64 B, in launch order, so one replay of
+ * a captured token graph leaves the whole step's per-workgroup timeline. Captured graphs
+ * are dropped (re-captured with the stamp pointers on the next graph decode); launches
+ * past bytes / (slot_wgs * 64) regions are not stamped. slot_wgs must cover the largest
+ * decode grid (the error names the bound). dev_buf NULL switches it off. */
+int llmi_engine_debug_timeline(llmi_engine* e, void* dev_buf, size_t bytes, int slot_wgs);
 /* Test hook: overwrite the device decode state's next position only (the host's copy is
  * left alone), to check that a host/device position mismatch is reported (error bit 4). */
 int llmi_engine_debug_set_next_pos(llmi_engine* e, int next_pos);

@@ -159,6 +159,15 @@ struct Engine {
     static constexpr int kPfSlabs = 8;
     int host_next_pos = 0, prompt_len = 0;
     unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
+    // llmi_engine_debug_timeline: every stamped launch of a recorded step gets its own
+    // region of dbg_stride workgroups (slot = launch order), dbg_slots regions in all
+    int dbg_stride = 0, dbg_slots = 0;
+    mutable int dbg_slot = 0;
+    unsigned long long* stamp_ptr() const {
+        if (!dbg_stamps || dbg_stride == 0) return dbg_stamps;
+        const int s = dbg_slot++;
+        return s < dbg_slots ? dbg_stamps + (size_t)s * dbg_stride * 8 : nullptr;
+    }
     uint64_t seed = 0;
     // stochastic sampling (Llama<T>::Sampling, llama.cpp:245-262): 0 = greedy argmax
     int sample_k = 0;
@@ -525,7 +534,7 @@ struct Engine {
     // ---------------------------------------------------------- one token
     GemvArgs lm_args(bool from_x = false) const {
         GemvArgs a;
-        a.stamps = dbg_stamps;
+        a.stamps = stamp_ptr();
         a.w = lm_head;
         a.w_dtype = edt;
         a.n_rows = vl;
@@ -549,7 +558,7 @@ struct Engine {
     GemvArgs qkv_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
-        a.stamps = dbg_stamps;
+        a.stamps = stamp_ptr();
         a.w = L.qkv; a.scales = L.qkv_s; a.w_dtype = wdt;
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
@@ -558,7 +567,7 @@ struct Engine {
     }
     AttnArgs attn_args(int l) const {
         AttnArgs a;
-        a.stamps = dbg_stamps;
+        a.stamps = stamp_ptr();
         const size_t eb = dtype_size(c.kv_dtype);
         a.qkv = qkv_buf;
         a.k_cache = (char*)kcache + (size_t)l * kv_layer_elems * eb;
@@ -581,7 +590,7 @@ struct Engine {
     OprojArgs o_args(int l) const {
         const Layer& L = layers[l];
         OprojArgs a;
-        a.stamps = dbg_stamps;
+        a.stamps = stamp_ptr();
         a.w = L.o; a.scales = L.o_s; a.w_dtype = wdt;
         a.head_major = 0;
         a.n_rows = c.hidden; a.ldw = ql;
@@ -594,7 +603,7 @@ struct Engine {
     GemvArgs gu_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
-        a.stamps = dbg_stamps;
+        a.stamps = stamp_ptr();
         a.w = L.gu; a.scales = L.gu_s; a.w_dtype = wdt;
         a.n_rows = 2 * il; a.k = c.hidden;
         a.x_fixed = xacc; a.x_out = x;  // residual after attention, written back to x by workgroup 0
@@ -608,7 +617,7 @@ struct Engine {
     GemvArgs down_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
-        a.stamps = dbg_stamps;
+        a.stamps = stamp_ptr();
         a.w = L.down; a.scales = L.down_s; a.w_dtype = wdt;
         a.n_rows = c.hidden; a.k = il; a.x = act;
         a.epi = EPI_ATOMIC; a.yacc = res[(l + 1) % 2];
@@ -718,6 +727,7 @@ struct Engine {
 
     int record_step() {
         LLMI_REQUIRE(!grouped, "engine: a group rank is stepped by its group");
+        dbg_slot = 0;
         LLMI_TRY(rec_start());
         for (int l = 0; l < c.layers; ++l) {
             LLMI_TRY(rec_attn(l));
@@ -1351,6 +1361,29 @@ int llmi_engine_debug_set_next_pos(llmi_engine* e, int next_pos) {
 int llmi_engine_debug_stamps(llmi_engine* e, void* dev_buf) {
     LLMI_REQUIRE(e, "debug_stamps: null engine");
     e->e.dbg_stamps = static_cast<unsigned long long*>(dev_buf);
+    return LLMI_OK;
+}
+
+int llmi_engine_debug_timeline(llmi_engine* e, void* dev_buf, size_t bytes, int slot_wgs) {
+    LLMI_REQUIRE(e, "debug_timeline: null engine");
+    Engine& g = e->e;
+    LLMI_HIP(hipSetDevice(g.device));
+    LLMI_HIP(hipStreamSynchronize(g.stream));
+    g.graphs.clear();  // the captured steps carry the stamp pointers: re-capture
+    if (!dev_buf) {
+        g.dbg_stamps = nullptr;
+        g.dbg_stride = g.dbg_slots = 0;
+        return LLMI_OK;
+    }
+    // every decode launch's grid must fit its region: GEMVs <= 1024 workgroups, attention
+    // heads x splits, o_proj heads x (hidden / 16 rows) at most
+    const int ns = (g.c.max_seq + llmi::kAttnChunk - 1) / llmi::kAttnChunk;
+    const int need = std::max(std::max(1024, g.hl * ns), g.hl * ((g.c.hidden + 15) / 16));
+    LLMI_REQUIRE(slot_wgs >= need, "debug_timeline: slot_wgs must be >= " + std::to_string(need));
+    g.dbg_stamps = static_cast<unsigned long long*>(dev_buf);
+    g.dbg_stride = slot_wgs;
+    g.dbg_slots = (int)std::min<size_t>(bytes / ((size_t)slot_wgs * 64), 1 << 20);
+    LLMI_REQUIRE(g.dbg_slots > 0, "debug_timeline: buffer smaller than one slot");
     return LLMI_OK;
 }
 

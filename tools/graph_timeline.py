@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Timeline of ONE graph-replayed decode token (rocprofv3 cannot trace graph replays on
+this image: profiles/r02_graph_trace_segfault.log). Every stamped launch of the captured
+step writes {start, end, CU} per workgroup into its own region (llmi_engine_debug_timeline,
+s_memrealtime at 100 MHz), so the replay itself reports each kernel's span (first
+workgroup start -> last workgroup end) and the gap to the next kernel's first workgroup --
+the in-graph kernel boundary that the eager traces can only infer.
+
+    python tools/graph_timeline.py [--ctx 8,512,1024,2047] [--layers 32] [--out f.json]
+
+Launch order per token: step_start (unstamped), then per layer qkv, attn, o, gate_up,
+down, then lm_head.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "llm-inference_amd"))
+from llmi import _lib  # noqa: E402
+from llmi.engine import Engine, preset, synth_prompt  # noqa: E402
+
+KINDS = ("qkv", "attn", "o", "gate_up", "down")
+
+
+def analyse(host, n_slots, stride, layers):
+    spans, starts, ends, names = [], [], [], []
+    for s in range(n_slots):
+        rows = host[s * stride:(s + 1) * stride]
+        v = rows[rows[:, 0] > 0].astype(np.int64)
+        if not len(v):
+            continue
+        names.append(KINDS[s % 5] if s < 5 * layers else "lm_head")
+        starts.append(v[:, 0].min())
+        ends.append(v[:, 3].max())
+    starts, ends = np.array(starts), np.array(ends)
+    t0 = starts[0]
+    span = (ends - starts) / 100.0
+    gap = (starts[1:] - ends[:-1]) / 100.0
+    out = {"launches": len(names), "token_us_first_start_to_last_end": round(float((ends[-1] - t0) / 100.0), 1),
+           "sum_spans_us": round(float(span.sum()), 1), "sum_gaps_us": round(float(gap.sum()), 1)}
+    per = {}
+    for k in KINDS + ("lm_head",):
+        idx = [i for i, n in enumerate(names) if n == k]
+        if not idx:
+            continue
+        g = [gap[i] for i in idx if i < len(gap)]
+        per[k] = {"n": len(idx), "span_us_mean": round(float(span[idx].mean()), 2),
+                  "span_us_min": round(float(span[idx].min()), 2), "span_us_max": round(float(span[idx].max()), 2),
+                  "gap_after_us_mean": round(float(np.mean(g)), 2) if g else None}
+    out["per_kernel"] = per
+    out["gap_us_quantiles"] = [round(float(x), 2) for x in np.quantile(gap, [0, 0.1, 0.5, 0.9, 1.0])]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ctx", default="8,512,1024,2047")
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--preset", default="llama2-7b")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    lib = _lib.lib()
+    cfg = preset(a.preset, layers=a.layers, max_seq=2048)
+    n_slots = 5 * a.layers + 1
+    ns = (cfg.max_seq + 63) // 64
+    stride = max(1024, cfg.heads * ns, cfg.heads * ((cfg.hidden + 15) // 16))
+    nbytes = n_slots * stride * 64
+    buf = C.c_void_p()
+    assert lib.llmi_device_alloc(C.byref(buf), C.c_size_t(nbytes)) == 0
+    host = np.zeros((n_slots * stride, 8), np.uint64)
+    res = {"preset": a.preset, "layers": a.layers, "slot_wgs": stride, "clock": "s_memrealtime 100 MHz",
+           "mode": "hipGraph replay (one captured graph per active split count)", "ctx": {}}
+    with Engine(cfg) as e:
+        e.load_synthetic(0)
+        e.set_prompt(synth_prompt(0, 8, cfg.vocab))
+        _lib.call("llmi_engine_debug_timeline", e._h, buf, C.c_size_t(nbytes), stride)
+        pos = 0
+        for c in sorted(int(x) for x in a.ctx.split(",")):
+            if c - 1 > pos:
+                e.decode(c - 1 - pos)  # graph replays up to the position before the stamped one
+                pos = c - 1
+            e.sync()
+            lib.llmi_device_memset(buf, 0, C.c_size_t(nbytes))
+            e.decode(1)  # the stamped replay: position c - 1, context c
+            pos += 1
+            e.sync()
+            lib.llmi_memcpy(host.ctypes.data_as(C.c_void_p), buf, C.c_size_t(nbytes), 1)
+            r = analyse(host, n_slots, stride, a.layers)
+            res["ctx"][str(c)] = r
+            print(c, json.dumps(r), flush=True)
+        lib.llmi_engine_debug_timeline(e._h, None, C.c_size_t(0), 0)
+    lib.llmi_device_free(buf)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
