@@ -124,10 +124,15 @@ int llmi_topk(const void* logits, int dtype, int rows, int vocab, int k, int32_t
 /* launchSampling (src/kernels/sampling.h:12-18, sampling.cu:28-115): for each row not yet
  * finished, topk_vals <- exp(v - v[0]) in place, threshold u * sum, output_id = the first id
  * whose running subtraction reaches <= 0 (% vocab), seqlen += 1, is_finished = (id == end_id).
- * u in (0, 1] is drawn from llmi-prng-v1 seeded by step, stream = row (the reference uses
- * curand XORWOW with the same seed/subsequence roles). is_finished: device uint8 (C++ bool). */
+ * u in (0, 1] is the reference's draw, curand_uniform of curand_init(step, row, 0): cuRAND's
+ * XORWOW restated (rows < 65536). is_finished: device uint8 (C++ bool). */
 int llmi_sampling(const int32_t* topk_ids, void* topk_vals, int dtype, int rows, int k, int32_t* output_id,
                   int32_t* seqlen, uint8_t* is_finished, int step, int end_id, int vocab, llmi_stream_t stream);
+
+/* The draw llmi_sampling makes, computed on the host (no device work): the first
+ * curand_uniform of curand_init(seed, subsequence, 0) -- cuRAND's XORWOW as restated in
+ * csrc/xorwow.h (subsequence < 65536). For checking the restatement against a CPU oracle. */
+int llmi_curand_uniform(uint64_t seed, uint32_t subsequence, float* out);
 
 /* launchRepeatKVCache (src/kernels/repeat_kv.h, repeat_kv.cu:7-91): caches [layers, batch,
  * kv_heads, max_seq, d] -> k_dst/v_dst [batch, heads, max_k_len, d], query head h reading kv
@@ -278,7 +283,9 @@ int llmi_engine_load_bin(llmi_engine* e, const char* weight_path);
 int llmi_engine_load_tensor(llmi_engine* e, const char* name, const float* host, size_t count);
 /* Llama<T>::Sampling (llama.cpp:245-262: launchTopKforBeamSearch + launchSampling) inside the
  * decode step: k in [1, 16] samples each generated token from the top k logits with
- * sampling.cu's rule, u drawn from llmi-prng-v1 at step = seed + (position of the token);
+ * sampling.cu's rule, u = curand_uniform(curand_init(step, 0, 0)) (cuRAND XORWOW restated)
+ * at step = seed + (tokens so far, the sampled token's position) (seed 0: the reference's step,
+ * llama.cpp:405-423);
  * k = 0 restores greedy argmax (the default). Needs tp_world == 1. Applies to tokens chosen
  * by decode steps (a batched prefill's first token stays greedy). */
 int llmi_engine_set_sampling(llmi_engine* e, int k, uint64_t seed);

@@ -17,19 +17,23 @@
 // tid 0 too). Semantics follow SamplingKernel (sampling.cu:28-84) exactly:
 // exp(v - v[0]) in place (stored as T), threshold = u * sum, first i whose running
 // subtraction reaches <= 0, ids taken % vocab, seqlen / is_finished update, rows already
-// finished untouched. The reference draws u with curand_uniform(XORWOW seeded by
-// step, subsequence = row); XORWOW's skip-ahead tables are not restated here, so u is
-// llmi-prng-v1: u = ((bits(tensor_key(step, SAMPLE), row) >> 40) + 1) * 2^-24 in (0, 1],
-// the same interval as curand_uniform. The oracle (oracle/sampling.py) uses the same
-// draw, so the selection is bit-exact against it.
+// finished untouched. u is the reference's own draw, curand_uniform of
+// curand_init(step, row, 0) -- cuRAND's XORWOW restated in xorwow.h (row > 0 jumps the
+// state by row * 2^67 steps through a GF(2) matrix table built here on the host); the
+// oracle (oracle/sampling.py over oracle/xorwow.py) makes the same draw, so the
+// selection is bit-exact against it.
+#include <array>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
 #include "kernels.h"
-#include "prng.h"
+#include "xorwow.h"
 
 namespace llmi {
 namespace {
 
 constexpr int kTopkThreads = 1024;
-constexpr uint32_t kSampleTid = 0x5A3Du;  // llmi-prng-v1 stream id of the sampling draw
 
 template <typename T> __device__ __forceinline__ float ldv(const T* p) { return (float)*p; }
 template <> __device__ __forceinline__ float ldv<__half>(const __half* p) { return __half2float(*p); }
@@ -98,7 +102,8 @@ __global__ __launch_bounds__(kTopkThreads) void topk_kernel(const T* __restrict_
 template <typename T>
 __global__ void sampling_kernel(const int32_t* __restrict__ topk_ids, T* __restrict__ topk_vals, int rows, int K,
                                 int32_t* __restrict__ output_id, int32_t* __restrict__ seqlen,
-                                uint8_t* __restrict__ is_finished, int step, int end_id, int vocab) {
+                                uint8_t* __restrict__ is_finished, int step, int end_id, int vocab,
+                                const uint32_t* __restrict__ jumps) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= rows || is_finished[b]) return;
     T* v = topk_vals + (size_t)b * K;
@@ -109,8 +114,10 @@ __global__ void sampling_kernel(const int32_t* __restrict__ topk_ids, T* __restr
         stv(v + i, expf(ldv(v + i) - mx));
         sum += ldv(v + i);
     }
-    const uint64_t r = prng::bits(prng::tensor_key((uint64_t)(int64_t)step, kSampleTid), (uint64_t)b);
-    float thr = (float)((r >> 40) + 1ull) * 0x1p-24f * sum;
+    // curand_init((unsigned long long)step, b, 0); curand_uniform (sampling.cu:66-69)
+    XorwowState rs = xorwow_init((uint64_t)(int64_t)step);
+    if (b > 0) xorwow_jump(rs, (uint32_t)b, jumps);
+    float thr = xorwow_uniform(xorwow_next(rs)) * sum;
     int out = id[0];
     for (int i = 0; i < K; ++i) {
         thr -= ldv(v + i);
@@ -133,9 +140,11 @@ __global__ void sample_pick_kernel(const DecodeState* st, const int32_t* __restr
             v[i] = expf(v[i] - mx);
             sum += v[i];
         }
+        // the reference's step = tokens so far (llama.cpp:405-423) = cur_pos + 1, offset by
+        // the caller's seed (0: the reference's stream); batch row 0: no subsequence jump
         const uint64_t step = seed + (uint64_t)(st->cur_pos + 1);
-        const uint64_t r = prng::bits(prng::tensor_key(step, kSampleTid), 0ull);
-        float thr = (float)((r >> 40) + 1ull) * 0x1p-24f * sum;
+        XorwowState rs = xorwow_init(step);
+        float thr = xorwow_uniform(xorwow_next(rs)) * sum;
         int out = ids[0];
         for (int i = 0; i < K; ++i) {
             thr -= v[i];
@@ -167,7 +176,61 @@ int topk_dispatch(const void* logits, int rows, int vocab, int k, int32_t* ids, 
     return LLMI_OK;
 }
 
+// columns of M^(2^67 * 2^i), i < kXorwowJumpBits, M the one-step map of the 160-bit v
+std::vector<uint32_t> build_jump_table() {
+    typedef std::array<uint32_t, 5> V;
+    std::vector<V> cols(160), next(160);
+    for (int c = 0; c < 160; ++c) {
+        XorwowState s{};
+        s.v[c >> 5] = 1u << (c & 31);
+        (void)xorwow_next(s);
+        for (int w = 0; w < 5; ++w) cols[c][w] = s.v[w];
+    }
+    auto square = [&]() {
+        for (int c = 0; c < 160; ++c) {
+            V r{};
+            for (int j = 0; j < 160; ++j)
+                if ((cols[c][j >> 5] >> (j & 31)) & 1u)
+                    for (int w = 0; w < 5; ++w) r[w] ^= cols[j][w];
+            next[c] = r;
+        }
+        cols.swap(next);
+    };
+    for (int i = 0; i < 67; ++i) square();
+    std::vector<uint32_t> t((size_t)kXorwowJumpBits * 160 * 5);
+    for (int i = 0; i < kXorwowJumpBits; ++i) {
+        for (int c = 0; c < 160; ++c)
+            for (int w = 0; w < 5; ++w) t[((size_t)i * 160 + c) * 5 + w] = cols[c][w];
+        if (i + 1 < kXorwowJumpBits) square();
+    }
+    return t;
+}
+
 }  // namespace
+
+const std::vector<uint32_t>& xorwow_host_table() {
+    static const std::vector<uint32_t> host = build_jump_table();  // thread-safe static init
+    return host;
+}
+
+const uint32_t* xorwow_jump_table() {
+    static std::mutex mu;
+    static std::unordered_map<int, uint32_t*> per_device;
+    std::lock_guard<std::mutex> lock(mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    auto it = per_device.find(dev);
+    if (it != per_device.end()) return it->second;
+    const std::vector<uint32_t>& host = xorwow_host_table();
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, host.size() * 4) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    per_device[dev] = d;
+    return d;
+}
 
 int sample_pick_launch(const DecodeState* st, const int32_t* ids, float* vals, int k, uint64_t seed,
                        unsigned long long* partials, int np, hipStream_t s) {
@@ -190,17 +253,36 @@ int sampling_launch(const int32_t* topk_ids, void* topk_vals, int dtype, int row
     LLMI_REQUIRE(topk_ids && topk_vals && output_id && seqlen && is_finished && rows > 0 && k >= 1 && vocab > 0,
                  "sampling: bad arguments");
     LLMI_REQUIRE(dtype == LLMI_F32 || dtype == LLMI_F16, "sampling: dtype must be f32 or f16");
+    LLMI_REQUIRE(rows <= (1 << kXorwowJumpBits), "sampling: at most 65536 rows (curand subsequence jumps)");
+    const uint32_t* jumps = nullptr;  // rows > 1 jump their curand state by row * 2^67
+    if (rows > 1) {
+        jumps = xorwow_jump_table();
+        LLMI_REQUIRE(jumps != nullptr, "sampling: cannot place the XORWOW jump table on the device");
+    }
     const int grid = (rows + kWave - 1) / kWave;
     if (dtype == LLMI_F32)
         hipLaunchKernelGGL(sampling_kernel<float>, dim3(grid), dim3(kWave), 0, s, topk_ids,
                            static_cast<float*>(topk_vals), rows, k, output_id, seqlen, is_finished, step, end_id,
-                           vocab);
+                           vocab, jumps);
     else
         hipLaunchKernelGGL(sampling_kernel<__half>, dim3(grid), dim3(kWave), 0, s, topk_ids,
                            static_cast<__half*>(topk_vals), rows, k, output_id, seqlen, is_finished, step, end_id,
-                           vocab);
+                           vocab, jumps);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }
 
 }  // namespace llmi
+
+// host-side restatement check (no device work): the first curand_uniform of
+// curand_init(seed, subsequence, 0), from the same xorwow.h code and jump table the
+// sampling kernel uses
+extern "C" int llmi_curand_uniform(uint64_t seed, uint32_t subsequence, float* out) {
+    using namespace llmi;
+    LLMI_REQUIRE(out, "curand_uniform: null output");
+    LLMI_REQUIRE(subsequence < (1u << kXorwowJumpBits), "curand_uniform: subsequence must be < 65536");
+    XorwowState s = xorwow_init(seed);
+    if (subsequence) xorwow_jump(s, subsequence, xorwow_host_table().data());
+    *out = xorwow_uniform(xorwow_next(s));
+    return LLMI_OK;
+}

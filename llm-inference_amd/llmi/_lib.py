@@ -90,6 +90,7 @@ _SIGS = {
     "llmi_engine_time_kernel": (_I, [_P, _I, _I, C.POINTER(_F), C.POINTER(_U64)]),
     "llmi_engine_debug_stamps": (_I, [_P, _P]),
     "llmi_engine_debug_timeline": (_I, [_P, _P, _SZ, _I]),
+    "llmi_curand_uniform": (_I, [_U64, _U32, C.POINTER(_F)]),
     "llmi_engine_debug_set_next_pos": (_I, [_P, _I]),
     "llmi_engine_xchg_handle": (_I, [_P, _P]),
     "llmi_engine_xchg_open": (_I, [_P, _P]),

@@ -11,18 +11,16 @@ Pinning: the reference's unit tests for these kernels print their outputs instea
 checking them (tests/unittests/test_topk.cu, test_sampling.cu, test_repeat_kv.cu), so
 there are no golden vectors; tests/test_sampling_oracle.py works the reference tests'
 own inputs (probs = arange, topk values K-1-(i%K), caches = arange) by hand. The
-sampling draw is build-defined: the reference's curand XORWOW stream is replaced by
-llmi-prng-v1 (`uniform` below), so sampling parity is against this restatement
-("parity unpinned" with respect to the reference's random stream; the selection rule
-given a draw follows sampling.cu:60-79).
+sampling draw is the reference's own, curand_uniform(curand_init(step, row, 0))
+(sampling.cu:66-69), restated in oracle/xorwow.py from cuRAND's published XORWOW (a
+CUDA toolkit header absent here): parity unpinned against cuRAND itself (no CUDA in
+this image), bit-exact between the device kernel and this restatement.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from . import prng
-
-SAMPLE_TID = 0x5A3D  # llmi-prng-v1 stream id of the sampling draw (csrc/sampling.hip)
+from . import xorwow
 
 
 def topk(logits: np.ndarray, k: int):
@@ -42,10 +40,8 @@ def topk(logits: np.ndarray, k: int):
 
 
 def uniform(step: int, row: int) -> np.float32:
-    """Draw in (0, 1] for (seed = step, stream = row); stands in for
-    curand_uniform(curand_init(step, row, 0)) at sampling.cu:62-64."""
-    b = prng.raw_bits(step, SAMPLE_TID, np.array([row], dtype=np.uint64))[0]
-    return np.float32((int(b) >> 40) + 1) * np.float32(2.0 ** -24)
+    """curand_uniform(curand_init(step, row, 0)) (sampling.cu:66-69), in (0, 1]."""
+    return xorwow.curand_uniform(int(step) & 0xFFFFFFFFFFFFFFFF, int(row))
 
 
 def sampling(topk_ids, topk_vals, seqlen, is_finished, step: int, end_id: int, vocab: int):

@@ -68,3 +68,40 @@ def test_c_abi_argument_checks():
     assert b"sampling" in L.llmi_last_error()
     assert L.llmi_repeat_kv(None, None, _lib.F16, 0, None, 1, 2, 4, 3, 2, 2, None, None, None) == -1
     assert b"repeat_kv" in L.llmi_last_error()
+
+
+def test_xorwow_restatement_properties():
+    """oracle/xorwow.py: the GF(2) one-step matrix reproduces curand()'s v update, a
+    2^5-step jump by 5 squarings equals 32 steps, and the subsequence jump composes
+    (jump(a) then jump(b) == jump(a + b) for disjoint bits)."""
+    from oracle import xorwow as X
+    cols = [X._v_step(1 << c) for c in range(160)]
+    v, d = X.init(12345)
+    x = X._pack(v)
+    assert X._apply(cols, x) == X._v_step(x)
+    c32 = cols
+    for _ in range(5):
+        c32 = X._square(c32)
+    y = x
+    for _ in range(32):
+        y = X._v_step(y)
+    assert X._apply(c32, x) == y
+    j = X.seq_jumps()
+    assert X._apply(j[1], X._apply(j[0], x)) == X._apply(j[0], X._apply(j[1], x))
+    v3, d3 = X.init_state(12345, 3)
+    assert X._pack(v3) == X._apply(j[1], X._apply(j[0], x)) and d3 == d
+
+
+def test_curand_uniform_c_abi_matches_oracle():
+    """llmi_curand_uniform (csrc/xorwow.h + the C++ jump table, host side) equals the
+    Python restatement bit for bit, for subsequences 0 (no jump) and > 0 (table)."""
+    import ctypes as C
+    from llmi import _lib
+    from oracle import xorwow as X
+    L = _lib.lib()
+    out = C.c_float()
+    for seed in (0, 1, 7, 512, 2047, 2 ** 40 + 3):
+        for sub in (0, 1, 2, 5, 255, 4096, 65535):
+            assert L.llmi_curand_uniform(seed, sub, C.byref(out)) == 0
+            assert np.float32(out.value) == X.curand_uniform(seed, sub), (seed, sub)
+    assert L.llmi_curand_uniform(0, 65536, C.byref(out)) == -1
