@@ -226,6 +226,18 @@ def int8_side(n_new: int = MAX_SEQ - PROMPT + 1):
             "gate_up_GBps": round(gu_b / (gu_us * 1e-6) / 1e9, 1)}
 
 
+def graph_timeline_side(eng, prompt, ctx: int = 1024):
+    """One token of the timed configuration (graph replay) stamped per workgroup
+    (llmi.timeline, llmi_engine_debug_timeline): kernel spans and in-graph boundaries at
+    context `ctx` -- the graph-mode counterpart of the eager HIP-event kernels_us."""
+    from llmi.timeline import stamped_token
+    eng.set_prompt(prompt)
+    r = stamped_token(eng, ctx - 1)
+    r["ctx"] = ctx
+    r["per_kernel_span_us"] = {k: v["span_us_mean"] for k, v in r.pop("per_kernel").items()}
+    return r
+
+
 def open_oneshot_exchange(eng, dist, prompt, world, n_check: int = 64):
     """Config 4's exchange: every rank maps every peer's inbox (IPC handles all-gathered
     over gloo), then a short greedy run over RCCL and over the one-shot peer exchange must
@@ -443,6 +455,12 @@ def main():
                 side["tp_exchange"]["oneshot_rejected"] = xchg["oneshot_rejected"]
         except Exception as e:  # reported, never fatal to the GPU number
             side["tp_exchange"] = {"error": repr(e)[:300]}
+    if world == 1 and not args.no_side and not args.eager:
+        progress("graph timeline side measurement")
+        try:
+            side["graph_timeline"] = graph_timeline_side(eng, prompt)
+        except Exception as e:  # reported, never fatal to the GPU number
+            side["graph_timeline"] = {"error": repr(e)[:300]}
     if world == 1 and not args.no_side:
         progress("prefill side measurement")
         side["prefill"] = prefill_side(eng, prompt_len=512)

@@ -23,39 +23,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "llm-inference_amd"))
 from llmi import _lib  # noqa: E402
 from llmi.engine import Engine, preset, synth_prompt  # noqa: E402
-
-KINDS = ("qkv", "attn", "o", "gate_up", "down")
-
-
-def analyse(host, n_slots, stride, layers):
-    spans, starts, ends, names = [], [], [], []
-    for s in range(n_slots):
-        rows = host[s * stride:(s + 1) * stride]
-        v = rows[rows[:, 0] > 0].astype(np.int64)
-        if not len(v):
-            continue
-        names.append(KINDS[s % 5] if s < 5 * layers else "lm_head")
-        starts.append(v[:, 0].min())
-        ends.append(v[:, 3].max())
-    starts, ends = np.array(starts), np.array(ends)
-    t0 = starts[0]
-    span = (ends - starts) / 100.0
-    gap = (starts[1:] - ends[:-1]) / 100.0
-    out = {"launches": len(names), "token_us_first_start_to_last_end": round(float((ends[-1] - t0) / 100.0), 1),
-           "sum_spans_us": round(float(span.sum()), 1), "sum_gaps_us": round(float(gap.sum()), 1)}
-    per = {}
-    for k in KINDS + ("lm_head",):
-        idx = [i for i, n in enumerate(names) if n == k]
-        if not idx:
-            continue
-        g = [gap[i] for i in idx if i < len(gap)]
-        per[k] = {"n": len(idx), "span_us_mean": round(float(span[idx].mean()), 2),
-                  "span_us_min": round(float(span[idx].min()), 2), "span_us_max": round(float(span[idx].max()), 2),
-                  "gap_after_us_mean": round(float(np.mean(g)), 2) if g else None}
-    out["per_kernel"] = per
-    out["gap_us_quantiles"] = [round(float(x), 2) for x in np.quantile(gap, [0, 0.1, 0.5, 0.9, 1.0])]
-    return out
-
+from llmi.timeline import analyse, slot_wgs  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
@@ -67,8 +35,7 @@ def main():
     lib = _lib.lib()
     cfg = preset(a.preset, layers=a.layers, max_seq=2048)
     n_slots = 5 * a.layers + 1
-    ns = (cfg.max_seq + 63) // 64
-    stride = max(1024, cfg.heads * ns, cfg.heads * ((cfg.hidden + 15) // 16))
+    stride = slot_wgs(cfg)
     nbytes = n_slots * stride * 64
     buf = C.c_void_p()
     assert lib.llmi_device_alloc(C.byref(buf), C.c_size_t(nbytes)) == 0

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Time the batched prefill (config 3: Llama-2-7B, 512 prompt rows) on one GPU,
-both GEMM precisions, and print JSON (ms, TFLOP/s on the algorithmic FLOPs)."""
+both GEMM precisions, and print JSON (ms, TFLOP/s on the algorithmic FLOPs).
+    python tools/prefill_probe.py [rows] [iters] [exact|fast]"""
 import json
 import os
 import sys
@@ -22,12 +23,13 @@ def prefill_flops(cfg, m):
 def main():
     m = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    modes = {"exact": (True,), "fast": (False,)}.get(sys.argv[3] if len(sys.argv) > 3 else "", (True, False))
     cfg = preset("llama2-7b", max_seq=m + 64)
     prompt = synth_prompt(1, m, cfg.vocab)
     out = {"m": m, "flops": prefill_flops(cfg, m)}
     with Engine(cfg) as e:
         e.load_synthetic(0)
-        for exact in (True, False):
+        for exact in modes:
             ts = []
             for i in range(iters + 1):
                 e.set_prompt(prompt)
