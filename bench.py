@@ -238,29 +238,35 @@ def graph_timeline_side(eng, prompt, ctx: int = 1024):
     return r
 
 
-def open_oneshot_exchange(eng, dist, prompt, world, n_check: int = 64):
+def open_oneshot_exchange(eng, dist, prompt, world, n_check: int = 64, rccl: bool = True):
     """Config 4's exchange: every rank maps every peer's inbox (IPC handles all-gathered
     over gloo), then a short greedy run over RCCL and over the one-shot peer exchange must
     give the same tokens on every rank before the one-shot path is used for the timed run;
     otherwise (or on any error, e.g. a peer that never arrives: error bit 8, no hang) the
-    run stays on RCCL and the JSON line says why."""
+    run stays on RCCL and the JSON line says why. Without RCCL (the one-device rehearsal,
+    LLMI_BENCH_ONE_DEVICE) the one-shot tokens must agree across the ranks, or it raises."""
     info = {"mode": "rccl"}
     ok, why = False, ""
+    tb = None
     try:
         hs = [None] * world
         dist.all_gather_object(hs, eng.xchg_handle())
         eng.xchg_open(hs)
-        ta = eng.generate(prompt, n_check)
+        ta = eng.generate(prompt, n_check) if rccl else None
         eng.set_exchange(1)
         tb = eng.generate(prompt, n_check)
-        ok = bool((ta == tb).all())
+        ok = True if ta is None else bool((ta == tb).all())
         why = "" if ok else "one-shot tokens differ from RCCL"
     except Exception as e:  # reported, never fatal: RCCL carries the run
         why = repr(e)[:300]
     oks = [None] * world
-    dist.all_gather_object(oks, (ok, why))
-    if all(o[0] for o in oks):
+    dist.all_gather_object(oks, (ok, why, None if tb is None else tb.tolist()))
+    if ok and not rccl and any(o[2] != oks[0][2] for o in oks):
+        ok = False
+    if all(o[0] for o in oks) and (rccl or all(o[2] == oks[0][2] for o in oks)):
         info["mode"] = "oneshot"
+    elif not rccl:
+        raise RuntimeError(f"one-device rehearsal: one-shot exchange failed: {[o[1] for o in oks]}")
     else:
         try:
             eng.set_exchange(0)
@@ -270,7 +276,7 @@ def open_oneshot_exchange(eng, dist, prompt, world, n_check: int = 64):
     return info
 
 
-def tp_exchange_side(eng, layers, ms_per_token, wbytes, mode="rccl"):
+def tp_exchange_side(eng, layers, ms_per_token, wbytes, mode="rccl", rccl=True):
     """TP exchange budget: per token 2 * layers int64 all-reduces of the
     hidden-size fixed-point residual (32 KB) plus one uint64 max over the lm_head
     partials. Times the engine's own residual all-reduce on its RCCL communicator --
@@ -279,9 +285,11 @@ def tp_exchange_side(eng, layers, ms_per_token, wbytes, mode="rccl"):
     ms per token and the per-rank weight stream."""
     out = {"calls_per_token": 2 * layers + 1, "payload_bytes": 4096 * 8}
     out["mode"] = mode
-    out["allreduce_us_eager"] = round(eng.time_kernel("allreduce", iters=200)[0], 2)
-    out["allreduce_us_graph"] = round(eng.time_kernel("allreduce_graph", iters=256)[0], 2)
-    lat = out["allreduce_us_graph"]
+    lat = None
+    if rccl:
+        out["allreduce_us_eager"] = round(eng.time_kernel("allreduce", iters=200)[0], 2)
+        out["allreduce_us_graph"] = round(eng.time_kernel("allreduce_graph", iters=256)[0], 2)
+        lat = out["allreduce_us_graph"]
     if mode == "oneshot":
         out["oneshot_us_eager"] = round(eng.time_kernel("xchg", iters=200)[0], 2)
         out["oneshot_us_graph"] = round(eng.time_kernel("xchg_graph", iters=256)[0], 2)
@@ -383,18 +391,23 @@ def main():
 
     dist = None
     tp_id = None
+    # one-device rehearsal of the N > 1 path (a one-GPU box): every rank on device 0, no RCCL
+    # (it refuses two ranks on one device), the one-shot exchange carries the TP reduction;
+    # the throughput is then N ranks sharing one GPU -- a path check, not a scaling number
+    one_dev = world > 1 and os.environ.get("LLMI_BENCH_ONE_DEVICE") == "1"
     if world > 1:
         import torch.distributed as dist  # plumbing only: id exchange, barrier, max
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        obj = [tp_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        tp_id = obj[0]
+        if not one_dev:
+            obj = [tp_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            tp_id = obj[0]
     elif args.tp_exchange:  # world-1 rehearsal: a single-rank RCCL communicator in the engine
         tp_id = tp_unique_id()
 
     cfg = preset("llama2-7b", max_seq=args.max_seq, tp_rank=rank, tp_world=world)
     cfg.kv_dtype = llmi.F16 if args.kv == "f16" else llmi.F32
-    eng = Engine(cfg, device=local, tp_id=tp_id)
+    eng = Engine(cfg, device=0 if one_dev else local, tp_id=tp_id)
     eng.load_synthetic(SEED)
     prompt = synth_prompt(SEED, PROMPT, cfg.vocab)
     n_fwd = cfg.max_seq
@@ -405,9 +418,11 @@ def main():
             dist.barrier()
 
     xchg = {"mode": "rccl" if tp_id is not None else "none"}
-    if dist is not None and os.environ.get("LLMI_TP_EXCHANGE", "oneshot") == "oneshot":
+    if dist is not None and (one_dev or os.environ.get("LLMI_TP_EXCHANGE", "oneshot") == "oneshot"):
         progress("one-shot peer exchange: open + check against RCCL")
-        xchg = open_oneshot_exchange(eng, dist, prompt, world)
+        xchg = open_oneshot_exchange(eng, dist, prompt, world, rccl=not one_dev)
+        if one_dev:
+            xchg["one_device_rehearsal"] = True
         progress(f"tp exchange: {xchg}")
 
     def one_generation():
@@ -446,11 +461,13 @@ def main():
     gu_us, gu_bytes = eng.time_kernel("gate_up", iters=256)
     kern = {k: eng.time_kernel(k, iters=128) for k in ("qkv", "attn", "o", "down", "lm_head")}
     side = {}
-    if tp_id is not None:
+    if tp_id is not None or one_dev:
         progress("tp exchange side measurement")
         try:
             side["tp_exchange"] = tp_exchange_side(eng, cfg.layers, elapsed * 1e3 / args.steps / n_fwd, wbytes,
-                                                   mode=xchg["mode"])
+                                                   mode=xchg["mode"], rccl=tp_id is not None)
+            if one_dev:
+                side["tp_exchange"]["one_device_rehearsal"] = True
             if "oneshot_rejected" in xchg:
                 side["tp_exchange"]["oneshot_rejected"] = xchg["oneshot_rejected"]
         except Exception as e:  # reported, never fatal to the GPU number
