@@ -88,6 +88,16 @@ int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llm
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m,
                 int n, int k, llmi_stream_t stream);
 
+/* One decode row through the HBM-streaming GEMV with its fused prologue/epilogue -- what
+ * LlamaSelfDecoder::forward strings together for a token (self_decoder.cpp:59-81 fused):
+ *   gamma != NULL: x is RMS-normalised and scaled by gamma (dtype gamma_dtype) first;
+ *   epilogue 0: y[n] = W x;  1: y[n] = W x + resid[n] (resid may not alias y);
+ *   2: W is [gate; up] (n = 2 inter rows), y[inter] = silu(W_gate x) * (W_up x).
+ * fp32 x / y / resid, W f16, f32 or i8 (+ scales). */
+int llmi_linear_fused(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int n, int k,
+                      const void* gamma, int gamma_dtype, float eps, int epilogue, const float* resid,
+                      llmi_stream_t stream);
+
 /* launchRoPE (src/kernels/qkv_bias_and_RoPE.h:40-42) for one decode token:
  * rotates q (heads) and k (kv_heads) of the fused qkv row [ (h + 2kv) * d ]
  * in place at position `pos` (= step - 1), pairs (i, i + d/2),

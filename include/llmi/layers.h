@@ -297,13 +297,26 @@ public:
           ffn(head_num, head_size, inter_size, stream, cublas_wrapper, allocator) {}
     ~LlamaSelfDecoder() {
         if (resid_ptr) allocator->Free(resid_ptr, false);
+        for (float* p : fbuf)
+            if (p) allocator->Free(p, false);
     }
 
     // self_decoder.cpp:23-89 for one token; inputs "decoder_input" [1, H], "step" and
     // "layer_id" (host int), "finished"; outputs "decoder_output", "all_k_cache", "all_v_cache"
     // (FP32 or FP16 caches, chosen by their dtype).
+    // A batch-1 token runs five launches per layer instead of the reference's ten (same math,
+    // fp32 activations): RMSNorm folded into the q/k/v GEMV, RoPE into the attention (which
+    // writes the KV slot), the residual adds into the o_proj / down GEMV epilogues, RMSNorm +
+    // SiLU * up into the gate_up GEMV (llmi_linear_fused). Other batch sizes go op by op.
     void forward(TensorMap& input_tensors, const std::vector<LlamaLayerWeight<T>*>& layerWeights,
                  TensorMap& output_tensors, LLaMAAttentionDynParams& dyn_params) {
+        if (dyn_params.batch_size == 1 && fused_ok(input_tensors, output_tensors)) {
+            llmi_detail::ActF32 din(input_tensors["decoder_input"], allocator, stream, true, "LlamaSelfDecoder");
+            llmi_detail::ActF32 dout(output_tensors["decoder_output"], allocator, stream, false, "LlamaSelfDecoder");
+            forward_fused(din.get(), dout.get(), input_tensors, output_tensors, layerWeights);
+            dout.store();
+            return;
+        }
         if (!resid_ptr) {
             resid_ptr = allocator->Malloc(resid_ptr, sizeof(float) * dyn_params.batch_size * hidden, false);
             decoder_residual = std::make_unique<TensorWrapper<float>>(GPU, FP32, std::vector<int>{dyn_params.batch_size, hidden}, resid_ptr);
@@ -339,6 +352,64 @@ public:
     }
 
 private:
+    bool fused_ok(TensorMap& in, TensorMap& out) {
+        Tensor* x = in["decoder_input"];
+        Tensor* k = out["all_k_cache"];
+        Tensor* v = out["all_v_cache"];
+        return x->size() == hidden && k->shape.size() == 5 && k->shape[1] == 1 && v->dtype == k->dtype &&
+               (k->dtype == FP32 || k->dtype == FP16);
+    }
+    float* scratch(int slot, size_t n) {
+        if (n > fcap[slot]) {
+            if (fbuf[slot]) allocator->Free(fbuf[slot], false);
+            fbuf[slot] = allocator->Malloc(fbuf[slot], n * sizeof(float), false);
+            fcap[slot] = n;
+        }
+        return fbuf[slot];
+    }
+    void forward_fused(TensorWrapper<float>* xin, TensorWrapper<float>* xout, TensorMap& in, TensorMap& out,
+                       const std::vector<LlamaLayerWeight<T>*>& lw) {
+        Tensor* kc = out["all_k_cache"];
+        Tensor* vc = out["all_v_cache"];
+        const int kv = kc->shape[2], max_seq = kc->shape[3], hd = kc->shape[4];
+        const int step = in["step"]->as<int>()->getVal();
+        LLM_CHECK_WITH_INFO(step >= 1 && step <= max_seq, "LlamaSelfDecoder: step out of the cache range");
+        LLM_CHECK_WITH_INFO((int)lw.size() >= num_layer, "LlamaSelfDecoder: fewer layer weights than layers");
+        const int wdt = llmiWeightDtype(getWeightType<T>());
+        const int cdt = kc->dtype == FP16 ? LLMI_F16 : LLMI_F32;
+        const float base = selfAttn.GetAttnStaticParams().rotary_embedding_base;
+        auto raw = [](Tensor* t) -> void* {
+            return t->dtype == FP16 ? (void*)t->as<half_t>()->data : (void*)t->as<float>()->data;
+        };
+        void* kd = raw(kc);
+        void* vd = raw(vc);
+        float* x = xin->data;
+        float* y = xout->data;
+        for (int l = 0; l < num_layer; ++l) {
+            LlamaLayerWeight<T>* w = lw[l];
+            const int qkv_rows = w->self_attn_weight.qkv.shape[0], inter = w->ffn_weight.down.shape[1];
+            const int heads = qkv_rows / hd - 2 * kv;
+            float* qkv = scratch(0, qkv_rows);
+            float* mha = scratch(1, (size_t)heads * hd);
+            float* r = scratch(2, hidden);
+            float* act = scratch(3, inter);
+            void* ws = llmi_detail::attn_workspace(heads, hd, max_seq);
+            // RMSNorm(x) . Wqkv^T; rope + KV slot step - 1 + masked MHA; r = x + o . Wo^T
+            LLMI_CALL(llmi_linear_fused(x, w->self_attn_weight.qkv.data, wdt, nullptr, qkv, qkv_rows, hidden,
+                                        w->attn_norm_weight.gamma, wdt, rmsnorm_eps, 0, nullptr, stream));
+            LLMI_CALL(llmi_attn_decode(qkv, kd, vd, cdt, l, max_seq, step - 1, heads, kv, hd, 1, base, mha,
+                                       ws, stream));
+            LLMI_CALL(llmi_linear_fused(mha, w->self_attn_weight.output.data, wdt, nullptr, r, hidden, heads * hd,
+                                        nullptr, wdt, 0.f, 1, x, stream));
+            // silu(RMSNorm(r) . Wg^T) * (RMSNorm(r) . Wu^T); out = r + act . Wd^T
+            LLMI_CALL(llmi_linear_fused(r, w->ffn_weight.gateAndup.data, wdt, nullptr, act, 2 * inter, hidden,
+                                        w->ffn_norm_weight.gamma, wdt, rmsnorm_eps, 2, nullptr, stream));
+            LLMI_CALL(llmi_linear_fused(act, w->ffn_weight.down.data, wdt, nullptr, y, hidden, inter, nullptr, wdt, 0.f,
+                                        1, r, stream));
+            x = y;
+        }
+    }
+
     int hidden, num_layer;
     float rmsnorm_eps;
     void* stream;
@@ -347,6 +418,8 @@ private:
     LLaMAFFNLayer<T> ffn;
     float* resid_ptr = nullptr;
     std::unique_ptr<TensorWrapper<float>> decoder_residual;
+    float* fbuf[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t fcap[4] = {0, 0, 0, 0};
 };
 
 // ------------------------------------------------------ context phase

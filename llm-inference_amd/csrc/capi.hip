@@ -81,6 +81,36 @@ int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales
     return LLMI_OK;
 }
 
+int llmi_linear_fused(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int n, int k,
+                      const void* gamma, int gamma_dtype, float eps, int epilogue, const float* resid,
+                      llmi_stream_t stream) {
+    LLMI_REQUIRE(x && w && y && n >= 1 && k >= 1, "linear_fused: null pointer or empty shape");
+    LLMI_REQUIRE(epilogue >= 0 && epilogue <= 2, "linear_fused: epilogue must be 0 (store), 1 (add) or 2 (silu_mul)");
+    LLMI_REQUIRE(epilogue != 1 || (resid && resid != y), "linear_fused: the add epilogue needs resid != y");
+    LLMI_REQUIRE(epilogue != 2 || n % 2 == 0, "linear_fused: silu_mul needs 2 * inter rows");
+    GemvArgs a;
+    a.w = w;
+    a.w_dtype = w_dtype;
+    a.scales = reinterpret_cast<const __half*>(w_scales);
+    a.n_rows = n;
+    a.k = k;
+    a.x = x;
+    a.gamma = gamma;
+    a.g_dtype = gamma_dtype;
+    a.eps = eps;
+    a.y = y;
+    if (epilogue == 0) {
+        a.epi = EPI_STORE;
+    } else if (epilogue == 1) {
+        a.epi = EPI_ADD;
+        a.resid = resid;
+    } else {
+        a.epi = EPI_SILU_MUL;
+        a.pair_off = n / 2;
+    }
+    return gemv_launch(a, STREAM(stream));
+}
+
 int llmi_rope_decode(float* qkv, int pos, int heads, int kv_heads, int head_dim, float base, llmi_stream_t stream) {
     return rope_decode_launch(qkv, pos, heads, kv_heads, head_dim, base, STREAM(stream));
 }

@@ -44,6 +44,7 @@ _SIGS = {
     "llmi_silu_mul": (_I, [_P, _P, _I, _I, _P]),
     "llmi_convert": (_I, [_P, _I, _P, _I, _SZ, _P]),
     "llmi_linear": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _P]),
+    "llmi_linear_fused": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _I, _F, _I, _P, _P]),
     "llmi_rope_decode": (_I, [_P, _I, _I, _I, _I, _F, _P]),
     "llmi_attn_workspace_bytes": (_SZ, [_I, _I, _I]),
     "llmi_attn_decode": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P]),
