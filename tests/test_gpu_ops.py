@@ -116,6 +116,38 @@ def test_linear_gemv(ops, wdt, n, k, m):
     assert rel(y, ref) < 2e-6
 
 
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("norm", [False, True])
+def test_linear_fused_epilogues(ops, epi, norm):
+    """llmi_linear_fused (the batch-1 LlamaSelfDecoder path): optional RMSNorm prologue with
+    an fp16 gamma, then store / + resid / silu(gate) * up, against float64 numpy."""
+    import ctypes as C
+    rng = np.random.default_rng(epi * 2 + int(norm))
+    k, inter = 4096, 1024
+    n = 2 * inter if epi == 2 else 1536
+    x = rng.standard_normal(k).astype(np.float32)
+    w = prng.linear_fp16(3, prng.layer_tid(1, prng.KIND_GATE), n, k)
+    g = (1.0 + 0.1 * rng.standard_normal(k)).astype(np.float16)
+    res = rng.standard_normal(n).astype(np.float32)
+    xn = x.astype(np.float64)
+    if norm:
+        xn = xn / np.sqrt(np.mean(xn * xn) + 1e-5) * g.astype(np.float64)
+    acc = w.astype(np.float64) @ xn
+    if epi == 0:
+        want = acc
+    elif epi == 1:
+        want = acc + res
+    else:
+        gate, up = acc[:inter], acc[inter:]
+        want = gate / (1.0 + np.exp(-gate)) * up
+    xt, wt, gt, rt = T(x), T(w), T(g), T(res)
+    y = torch.zeros(len(want), dtype=torch.float32, device=DEV)
+    _lib.call("llmi_linear_fused", C.c_void_p(xt.data_ptr()), C.c_void_p(wt.data_ptr()), _lib.F16, None,
+              C.c_void_p(y.data_ptr()), n, k, C.c_void_p(gt.data_ptr()) if norm else None, _lib.F16, 1e-5, epi,
+              C.c_void_p(rt.data_ptr()) if epi == 1 else None, None)
+    assert rel(N(y), want) < 2e-6
+
+
 def test_linear_golden_q_proj(ops):
     f = np.load(os.path.join(G, "f1_ops.npz"))
     w = prng.linear_fp16(int(f["seed"]), prng.layer_tid(0, prng.KIND_Q), 256, 4096)

@@ -69,6 +69,11 @@ def test_errors_are_codes_with_messages():
     assert "[llmi][ERROR]" in L.llmi_last_error().decode()
     rc = L.llmi_synth_fill_host(None, _lib.F32, _lib.SYN_INT8, 0, 0, 1, 1, 0, 0, 0)
     assert rc == -1 and b"int8" in L.llmi_last_error()
+    x = C.c_void_p(16)  # never dereferenced: the checks come first
+    rc = L.llmi_linear_fused(x, x, _lib.F16, None, x, 8, 64, None, _lib.F16, 1e-5, 3, None, None)
+    assert rc == -1 and b"epilogue" in L.llmi_last_error()
+    rc = L.llmi_linear_fused(x, x, _lib.F16, None, x, 8, 64, None, _lib.F16, 1e-5, 1, x, None)
+    assert rc == -1 and b"resid != y" in L.llmi_last_error()
     cfg = preset("tiny", tp_world=3)
     h = C.c_void_p()
     rc = L.llmi_engine_create(C.byref(cfg), 0, None, C.byref(h))
