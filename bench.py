@@ -180,7 +180,10 @@ def prefill_side(eng, prompt_len: int = 512, reps: int = 3):
     ids = synth_prompt(SEED + 1, m, cfg.vocab)
     out = {"config": f"Llama-2-7B fp16 prefill, {m} rows, batch 1 (BASELINE.json configs[2])",
            "flops": flops, "peak_tflops": MFMA_F16_PEAK_TFLOPS}
-    for exact in (True, False):
+    eng.set_prompt(ids)
+    eng.prefill(m, 2)  # the e4m3 weight copies are made on the first exact=2 call (not timed)
+    eng.sync()
+    for exact in (1, 2, 0):
         best = None
         for _ in range(reps):
             eng.set_prompt(ids)
@@ -191,9 +194,13 @@ def prefill_side(eng, prompt_len: int = 512, reps: int = 3):
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
         tf = flops / best / 1e12
-        out["exact" if exact else "fp16_activations"] = {
+        # exact: hi + lo fp16 planes (2x the fp16 MFMA work); exact_fp8lo: fp16 hi + e4m3 lo
+        # planes on the block-scaled fp8 MFMA (1.5x; F6 logits 1.16e-4 vs 1.14e-4 exact);
+        # fp16_activations: hi plane only
+        key = {1: "exact", 2: "exact_fp8lo", 0: "fp16_activations"}[exact]
+        out[key] = {
             "ms": round(best * 1e3, 3), "tflops": round(tf, 1), "frac_of_peak": round(tf / MFMA_F16_PEAK_TFLOPS, 4),
-            "mfma_work_factor": 2 if exact else 1}
+            "mfma_work_factor": {1: 2, 2: 1.5, 0: 1}[exact]}
     return out
 
 

@@ -107,6 +107,19 @@ __device__ __forceinline__ uint4 ld_nt16(const void* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// fp8 lo plane of the prefill GEMMs (split mode 3, gemm3.hip): an fp32 activation
+// a = hi + lo with hi = fp16(a) and |lo| <= 2^-11 |a|; lo is kept as OCP e4m3 of
+// lo * 2^kLo8Exp, clamped to +-448 (an element whose scaled lo would overflow, |a| >
+// ~224, keeps only its hi: the fp16-activation precision). The GEMM's block-scaled fp8
+// MFMA undoes the scale through its E8M0 operand scale (127 - kLo8Exp).
+constexpr int kLo8Exp = 12;
+__device__ __forceinline__ uint32_t lo8_pack4(float l0, float l1, float l2, float l3) {
+    auto c = [](float v) { return fminf(fmaxf(v * (float)(1 << kLo8Exp), -448.f), 448.f); };
+    int r = __builtin_amdgcn_cvt_pk_fp8_f32(c(l0), c(l1), 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(c(l2), c(l3), r, true);
+    return (uint32_t)r;
+}
+
 // Debug timeline (diagnostics only; a null base costs one scalar compare): per
 // workgroup 8 u64 at base + 8 * linear block id: [0] start, [1]/[2] kernel-defined
 // marks, [3] end, [4] __smid() -- 100 MHz s_memrealtime clock.

@@ -157,6 +157,13 @@ struct Engine {
     static constexpr int kPfSplit = 2;   // o_proj (gemm2) K slices
     static constexpr int kPfDown = 8;    // down (gemm3) K slices
     static constexpr int kPfSlabs = 8;
+    // split mode 3: e4m3 copies of the prefill GEMM weights (W * 2^exp, gemm3.hip), made on first use
+    struct W8Layer {
+        void *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
+        int qkv_e = 0, o_e = 0, gu_e = 0, down_e = 0;
+    };
+    std::vector<W8Layer> w8l;
+    char* w8blob = nullptr;
     int host_next_pos = 0, prompt_len = 0;
     unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
     // llmi_engine_debug_timeline: every stamped launch of a recorded step gets its own
@@ -189,6 +196,7 @@ struct Engine {
         if (vcache) (void)hipFree(vcache);
         if (scratch) (void)hipFree(scratch);
         if (pf) (void)hipFree(pf);
+        if (w8blob) (void)hipFree(w8blob);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
@@ -497,6 +505,12 @@ struct Engine {
     // Llama<T>::loadWeights(weight_path): weight_path + "<name>.bin" for every tensor.
     int load_bin(const char* weight_path) {
         LLMI_REQUIRE(weight_path, "load_bin: null path");
+        if (w8blob) {  // the fp8 copies follow the weights: rebuilt at the next split-3 prefill
+            LLMI_HIP(hipStreamSynchronize(stream));
+            LLMI_HIP(hipFree(w8blob));
+            w8blob = nullptr;
+            w8l.clear();
+        }
         std::vector<std::string> names = {"model.norm.weight", "lm_head.weight", "model.embed_tokens.weight"};
         for (int l = 0; l < c.layers; ++l)
             for (const char* leaf : {"input_layernorm.weight", "post_attention_layernorm.weight",
@@ -818,6 +832,39 @@ struct Engine {
         return LLMI_OK;
     }
 
+    // split mode 3 needs the fp8 lo pass of gemm3 on all four GEMMs (K multiples of 128)
+    bool lo8_supported() const {
+        return wdt == LLMI_F16 && c.kv_dtype == LLMI_F16 && gemm3_supported(ql + 2 * kvrows, c.hidden, EPI_SLAB, 2) &&
+               gemm3_supported(c.hidden, ql, EPI_SLAB, kPfDown) && gemm3_supported(2 * il, c.hidden, EPI_SILU_MUL, 1) &&
+               gemm3_supported(c.hidden, il, EPI_SLAB, kPfDown) && c.hidden % 128 == 0 && ql % 128 == 0 &&
+               il % 128 == 0 && ql / 128 >= kPfDown && il / 128 >= kPfDown;
+    }
+    int alloc_w8() {
+        if (w8blob) return LLMI_OK;
+        // e4m3 rows keep the fp16 row stride (2 K bytes, the first K used: gemm3.hip)
+        const int H = c.hidden;
+        const size_t nq = (size_t)(ql + 2 * kvrows) * H * 2, no = (size_t)H * ql * 2, ng = (size_t)2 * il * H * 2,
+                     nd = (size_t)H * il * 2;
+        auto al = [](size_t b) { return align_up(b, 256); };
+        const size_t per = al(nq) + al(no) + al(ng) + al(nd);
+        LLMI_HIP(hipMalloc(&w8blob, per * layers.size()));
+        w8l.assign(layers.size(), W8Layer{});
+        for (size_t l = 0; l < layers.size(); ++l) {
+            char* p = w8blob + l * per;
+            W8Layer& w = w8l[l];
+            w.qkv = p; p += al(nq);
+            w.o = p; p += al(no);
+            w.gu = p; p += al(ng);
+            w.down = p;
+            LLMI_TRY(w8_prepare(layers[l].qkv, ql + 2 * kvrows, H, w.qkv, &w.qkv_e, stream));
+            LLMI_TRY(w8_prepare(layers[l].o, H, ql, w.o, &w.o_e, stream));
+            LLMI_TRY(w8_prepare(layers[l].gu, 2 * il, H, w.gu, &w.gu_e, stream));
+            LLMI_TRY(w8_prepare(layers[l].down, H, il, w.down, &w.down_e, stream));
+        }
+        LLMI_HIP(hipStreamSynchronize(stream));
+        return LLMI_OK;
+    }
+
     // One prefill layer on the LDS-DMA GEMM (gemm2.hip): RMSNorm + split into fp16
     // planes, q/k/v GEMM, rope + KV write + causal attention, split, o_proj (+residual),
     // RMSNorm + split, gate_up GEMM writing silu(g) * u as planes, down (+residual).
@@ -825,15 +872,19 @@ struct Engine {
         const Layer& L = layers[l];
         const int H = c.hidden;
         const size_t eb = dtype_size(c.kv_dtype);
-        _Float16* lo = split == 2 ? pf_al : nullptr;
+        // split 3: the lo planes are e4m3 bytes against the e4m3 weight copies (gemm3.hip)
+        const bool f8 = split == 3;
+        const W8Layer* W8 = f8 ? &w8l[l] : nullptr;
+        _Float16* lo = split >= 2 ? pf_al : nullptr;
         Gemm2Args g;
-        g.a[0] = pf_ah; g.a[1] = lo; g.planes = split; g.m = m;
+        g.a[0] = pf_ah; g.a[1] = lo; g.planes = split >= 2 ? 2 : 1; g.m = m; g.lo8 = f8 ? 1 : 0;
         // (previous down slices into x) + rmsnorm + qkv
         LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.attn_norm, edt, c.rms_eps, pf_ah, lo, H, stream,
-                                   pf_pending ? pf_slab : nullptr, pf_pending));
+                                   pf_pending ? pf_slab : nullptr, pf_pending, f8));
         pf_pending = 0;
         g.lda = H; g.w = L.qkv; g.n = ql + 2 * kvrows; g.k = H;
         g.ldy = g.n;
+        if (f8) { g.w8 = W8->qkv; g.w8_exp = W8->qkv_e; }
         const bool qkv3 = gemm3_supported(g.n, H, EPI_SLAB, 2);
         if (qkv3) {  // two K slices (96 tiles alone would leave most CUs idle)
             g.epi = EPI_SLAB; g.ksplit = 2; g.slab = pf_qkv;
@@ -851,28 +902,37 @@ struct Engine {
         pa.cache_dtype = c.kv_dtype; pa.max_seq = c.max_seq; pa.m = m; pa.p0 = p0;
         pa.heads = hl; pa.kv_heads = kvl; pa.head_dim = c.head_dim; pa.rope_tab = rope_tab; pa.out = pf_o;
         if (c.kv_dtype == LLMI_F16) {  // MFMA attention writes the o_proj input planes itself
-            pa.mfma_planes = split; pa.out_hi = pf_ah; pa.out_lo = lo;
+            pa.mfma_planes = split >= 2 ? 2 : 1; pa.out_hi = pf_ah; pa.out_lo = lo; pa.out_lo8 = f8 ? 1 : 0;
             pa.split_ws = pf_split; pa.split_ws_floats = pf_split_floats;
         }
         LLMI_TRY(prefill_attn_launch(pa, stream));
         // o_proj + residual
-        if (c.kv_dtype != LLMI_F16) LLMI_TRY(rows_split_launch(pf_o, ql, m, ql, nullptr, edt, 0.f, pf_ah, lo, ql, stream));
+        if (c.kv_dtype != LLMI_F16)
+            LLMI_TRY(rows_split_launch(pf_o, ql, m, ql, nullptr, edt, 0.f, pf_ah, lo, ql, stream, nullptr, 0, f8));
         // split-K into slabs (128 tiles alone would leave half the CUs idle); the next
-        // rows_split adds the slices into x in slice order (deterministic)
-        const int so = (ql % (kPfSplit * 64)) == 0 ? kPfSplit : 1;
+        // rows_split adds the slices into x in slice order (deterministic). The fp8 lo
+        // pass is gemm3's: 8 slices of 256 x 256 tiles (256 workgroups)
+        int so = (ql % (kPfSplit * 64)) == 0 ? kPfSplit : 1;
         g.lda = ql; g.w = L.o; g.w_kblock = 0; g.n = H; g.k = ql;
         g.epi = EPI_SLAB; g.ksplit = so; g.slab = pf_slab; g.y = pf_x; g.ldy = H;
-        LLMI_TRY(gemm2_launch(g, stream));
+        if (f8) {
+            so = kPfDown; g.ksplit = so; g.w8 = W8->o; g.w8_exp = W8->o_e;
+            LLMI_TRY(gemm3_launch(g, stream));
+        } else {
+            LLMI_TRY(gemm2_launch(g, stream));
+        }
         g.w_kblock = 0;
         // (o slices into x) + rmsnorm + gate_up + silu * up -> planes of the down GEMM's input
-        LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.ffn_norm, edt, c.rms_eps, pf_ah, lo, H, stream, pf_slab, so));
+        LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.ffn_norm, edt, c.rms_eps, pf_ah, lo, H, stream, pf_slab, so, f8));
         g.lda = H; g.w = L.gu; g.n = 2 * il; g.k = H;
-        g.epi = EPI_SILU_MUL; g.pair_off = il; g.y = nullptr; g.y_hi = pf_act_h(); g.y_lo = split == 2 ? pf_act_l() : nullptr;
+        if (f8) { g.w8 = W8->gu; g.w8_exp = W8->gu_e; }
+        g.epi = EPI_SILU_MUL; g.pair_off = il; g.y = nullptr; g.y_hi = pf_act_h(); g.y_lo = split >= 2 ? pf_act_l() : nullptr;
         g.ldy = il;
         LLMI_TRY(gemm3_supported(g.n, H, EPI_SILU_MUL, 1) ? gemm3_launch(g, stream) : gemm2_launch(g, stream));
         // down + residual: K slices into slabs (gemm3: 8 uneven slices, 256 workgroups)
-        g.a[0] = pf_act_h(); g.a[1] = split == 2 ? pf_act_l() : nullptr;
+        g.a[0] = pf_act_h(); g.a[1] = split >= 2 ? pf_act_l() : nullptr;
         g.lda = il; g.w = L.down; g.n = H; g.k = il;
+        if (f8) { g.w8 = W8->down; g.w8_exp = W8->down_e; }
         g.epi = EPI_SLAB; g.pair_off = 0; g.y = pf_x; g.y_hi = g.y_lo = nullptr; g.ldy = H; g.slab = pf_slab;
         int sd;
         if (gemm3_supported(H, il, EPI_SLAB, kPfDown)) {
@@ -900,7 +960,8 @@ struct Engine {
         LLMI_REQUIRE(!grouped && c.tp_world == 1, "prefill: tensor-parallel prefill is not supported");
         LLMI_REQUIRE(prompt_len > 0, "prefill: set_prompt first");
         LLMI_REQUIRE(n >= 1 && host_next_pos + n <= prompt_len, "prefill: rows must lie inside the prompt");
-        LLMI_REQUIRE(split == 1 || split == 2, "prefill: split must be 1 (fp16 A) or 2 (fp32-faithful)");
+        LLMI_REQUIRE(split >= 1 && split <= 3,
+                     "prefill: split must be 1 (fp16 A), 2 (fp32-faithful) or 3 (fp16 hi + fp8 lo planes)");
         if (!gemm_supported(wdt, ql + 2 * kvrows, c.hidden, EPI_STORE) || !gemm_supported(wdt, c.hidden, ql, EPI_ADD) ||
             !gemm_supported(wdt, 2 * il, c.hidden, EPI_SILU_MUL) || !gemm_supported(wdt, c.hidden, il, EPI_ADD))
             return decode(n, 1);  // fp32 weights / odd shapes: the decode kernels, one row at a time
@@ -908,6 +969,8 @@ struct Engine {
         const bool use_gemm2 = wdt == LLMI_F16 && gemm2_supported(ql + 2 * kvrows, c.hidden, EPI_STORE) &&
                                gemm2_supported(c.hidden, ql, EPI_ADD) && gemm2_supported(2 * il, c.hidden, EPI_SILU_MUL) &&
                                gemm2_supported(c.hidden, il, EPI_ADD) && c.head_dim % 64 == 0;
+        if (split == 3 && !(use_gemm2 && lo8_supported())) split = 2;  // shapes without the fp8 lo pass: exact planes
+        if (split == 3) LLMI_TRY(alloc_w8());
         const int H = c.hidden, p_begin = host_next_pos;
         const size_t eb = dtype_size(c.kv_dtype);
         for (int p0 = p_begin; p0 < p_begin + n; p0 += pf_rows) {
@@ -920,7 +983,7 @@ struct Engine {
                     continue;
                 }
                 GemmArgs g;
-                g.split = split;
+                g.split = split == 3 ? 2 : split;
                 g.w_dtype = wdt;
                 g.m = m;
                 // rmsnorm + qkv
@@ -1239,7 +1302,7 @@ int llmi_engine_decode(llmi_engine* e, int n_steps, int use_graph) {
 int llmi_engine_prefill(llmi_engine* e, int n_tokens, int exact) {
     LLMI_REQUIRE(e, "null engine");
     LLMI_HIP(hipSetDevice(e->e.device));
-    return e->e.prefill(n_tokens, exact ? 2 : 1);
+    return e->e.prefill(n_tokens, exact == 2 ? 3 : exact ? 2 : 1);
 }
 
 int llmi_engine_sync(llmi_engine* e) {

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kThreads) void gemm2_kernel(Gemm2Args a) {
 template <int NPT, int KS>
 __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx, int k, const void* gamma,
                                                              int g_dtype, float eps, _Float16* hi, _Float16* lo,
-                                                             int ldh, const float* slab, int ksplit, int m) {
+                                                             int ldh, const float* slab, int ksplit, int m, int lo8) {
     __shared__ float red[16];
     float* xr = x + (size_t)blockIdx.x * ldx;
     const int k4 = k / 4;
@@ -304,7 +304,11 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
             l[q] = (_Float16)(e[q] - (float)h[q]);
         }
         reinterpret_cast<h4*>(hr)[j] = h;
-        if (lr) reinterpret_cast<h4*>(lr)[j] = l;
+        if (lr && lo8)  // e4m3 bytes of the exact fp32 remainder
+            reinterpret_cast<uint32_t*>(lr)[j] =
+                lo8_pack4(e[0] - (float)h[0], e[1] - (float)h[1], e[2] - (float)h[2], e[3] - (float)h[3]);
+        else if (lr)
+            reinterpret_cast<h4*>(lr)[j] = l;
     }
 }
 
@@ -376,7 +380,7 @@ int gemm2_launch(Gemm2Args a, hipStream_t s) {
 }
 
 int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,
-                      _Float16* lo, int ldh, hipStream_t s, const float* slab, int ksplit) {
+                      _Float16* lo, int ldh, hipStream_t s, const float* slab, int ksplit, bool lo8) {
     LLMI_REQUIRE(x && (hi || slab) && m > 0 && k > 0 && k % 4 == 0 && ldx % 4 == 0 && ldh % 4 == 0,
                  "rows_split: bad arguments");
     LLMI_REQUIRE(!slab || (ksplit >= 1 && ldx == k), "rows_split: slab rows must be dense (ldx == k)");
@@ -386,7 +390,7 @@ int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_
     const int ks = !slab ? 0 : (ksplit == 2 || (ksplit == 8 && npt <= 5)) ? ksplit : 0;
 #define RS_LAUNCH(N, S) \
     hipLaunchKernelGGL((rows_split_kernel<N, S>), dim3(m), dim3(kThreads), 0, s, x, ldx, k, gamma, g_dtype, eps, hi, lo, \
-                       ldh, slab, ksplit, m)
+                       ldh, slab, ksplit, m, lo8 ? 1 : 0)
 #define RS_KS(N) \
     do {                                  \
         if (ks == 2)                      \

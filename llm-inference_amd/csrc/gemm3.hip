@@ -33,7 +33,20 @@
 // conflicted fragment reads, -5..-10 %).
 // Exact mode (planes = 2): the lo plane is 2 K more K -- the K loop runs over
 // [hi | lo] against [W | W], so LDS and registers are those of the fp16 mode.
+// fp8 lo mode (lo8, split mode 3): the lo plane is e4m3(lo * 2^12) against an e4m3
+// copy of W (w8 = e4m3(W * 2^w8_exp)); both keep the byte stride of their fp16 form
+// (2 lda, 2 K per row, the first half used), so the per-thread DMA offsets serve both
+// passes. One 128-deep K tile per 128-B LDS row -- the
+// DMA, swizzle and fragment reads of an fp16 tile unchanged: a lane's two 16-B reads
+// (kk = 0, 1) become one 32-B operand of v_mfma_scale_f32_16x16x128_f8f6f4 (A and B
+// take the same lane/byte -> k map, so the sum over k is the same whatever order the
+// instruction assigns), the E8M0 operand scales 2^-12 and 2^-w8_exp undo the scaling.
+// At twice the fp16 MFMA rate and half the K tiles, the lo pass costs half of the
+// fp16 one; |lo| <= 2^-11 |a| and e4m3's 2^-4 steps leave ~2^-15 of |a W| per product.
 // Roofline: MFMA (fp16 dense 2.5 PFLOP/s); FLOPs per launch 2 * M * N * K * planes.
+#include <cstring>
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace llmi {
@@ -42,6 +55,9 @@ namespace {
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+typedef int i8v __attribute__((ext_vector_type(8)));
+
 
 constexpr int kT = 512;              // 8 waves: (wr, wc) = (w >> 2, w & 3)
 constexpr int kTile = 256;           // BM = BN
@@ -73,6 +89,16 @@ __device__ __forceinline__ void glds(const void* g, unsigned lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+// the same with a uniform base in SGPRs and a 32-bit per-lane byte offset (saddr form):
+// no 64-bit per-lane pointers to keep live across the K loop
+__device__ __forceinline__ void glds_s(const void* sbase, unsigned voff, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds)
                  : "memory");
 }
 
@@ -111,14 +137,19 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
     const int rt = tile % m_tiles, ct = tile / m_tiles;
     const int m0 = rt * kTile;
     // slice s covers K tiles [s * KT_all / S, (s + 1) * KT_all / S) of each plane
-    const int KT_all = a.k / kK;
-    const int kt0 = slice * KT_all / S;
-    const int KTs = (slice + 1) * KT_all / S - kt0;  // K tiles per plane in this slice
-    const int KT = KTs * a.planes;                   // virtual K tiles ([hi | lo])
+    // (lo8: on 128-deep boundaries, so the slice's fp8 lo tiles are whole)
+    const bool lo8 = a.lo8 != 0;
+    const int KT_all = lo8 ? a.k / (2 * kK) : a.k / kK;
+    const int kt0 = (lo8 ? 2 : 1) * (slice * KT_all / S);
+    const int KTs = (lo8 ? 2 : 1) * ((slice + 1) * KT_all / S) - kt0;  // 64-deep K tiles per plane in this slice
+    const int KT = lo8 ? KTs + KTs / 2 : KTs * a.planes;                // virtual K tiles ([hi | lo])
 
     // per-thread DMA sources: instruction i of a half-image fills half-local bytes
     // i * 8192 + 16 t, which hold logical byte swz3(.) of the image
-    size_t a_off[2][2], b_off[2][2];
+    // byte offsets < 4 GiB (checked by the launcher): half the VGPRs of size_t; W half 1 is
+    // W half 0 + a uniform row offset (gate_up: the up rows, else 128 rows on), never clamped
+    unsigned a_off[2][2], b_off[2];
+    const unsigned b_half1 = (unsigned)(EPI == EPI_SILU_MUL ? a.pair_off : 128) * (unsigned)a.k * 2u;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int b = swz3(i * kT * 16 + t * 16);
@@ -126,18 +157,18 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int m = min(m0 + h * 128 + row, a.m - 1);
-            a_off[h][i] = (size_t)m * a.lda * 2 + cb;
-            int n;
-            if (EPI == EPI_SILU_MUL)  // W half 0: gate columns g0 + row, half 1: their up rows
-                n = ct * 128 + row + (h ? a.pair_off : 0);
-            else
-                n = ct * kTile + h * 128 + row;
-            b_off[h][i] = (size_t)n * a.k * 2 + cb;
+            a_off[h][i] = (unsigned)m * (unsigned)a.lda * 2u + (unsigned)cb;
         }
+        // W half 0: gate columns g0 + row (gate_up) or tile rows 0-127
+        const int n = (EPI == EPI_SILU_MUL) ? ct * 128 + row : ct * kTile + row;
+        b_off[i] = (unsigned)n * (unsigned)a.k * 2u + (unsigned)cb;
     }
     const char* abase[2] = {reinterpret_cast<const char*>(a.a[0]),
                             reinterpret_cast<const char*>(a.planes == 2 ? a.a[1] : a.a[0])};
     const char* wbase = reinterpret_cast<const char*>(a.w);
+    const char* w8base = reinterpret_cast<const char*>(a.w8);
+    // E8M0 operand scales of the fp8 lo pass in one register: byte 0 for A (2^-12), byte 1 for B (2^-w8_exp)
+    const int sc = (127 - kLo8Exp) | ((127 - a.w8_exp) << 8);
     const unsigned lds0 = (unsigned)(uintptr_t)lds;
 
     // issue the half-image `half` (0 A0, 1 A1, 2 B0, 3 B1) of virtual K tile v
@@ -147,12 +178,15 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
         if (v >= 2) return;
 #endif
         const int plane = v >= KTs ? 1 : 0;
-        const size_t k0b = (size_t)(kt0 + v - plane * KTs) * kK * 2;
         const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (v & 1) * kBuf + half * kHalf + w * 1024);
+        // fp8 rows keep the fp16 rows' byte stride (the first half of each row is used),
+        // so the per-thread offsets serve both passes -- no second set of registers
+        const unsigned k0b = (lo8 && plane) ? (unsigned)(kt0 / 2 + v - KTs) * 128u : (unsigned)(kt0 + v - plane * KTs) * kK * 2u;
+        const char* base = half < 2 ? abase[plane] : (lo8 && plane) ? w8base : wbase;  // uniform
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const char* src = half < 2 ? abase[plane] + a_off[half][i] + k0b : wbase + b_off[half - 2][i] + k0b;
-            glds(src, dst + i * kT * 16);
+            const unsigned off = half < 2 ? a_off[half][i] + k0b : b_off[i] + (half == 3 ? b_half1 : 0u) + k0b;
+            glds_s(base, off, dst + i * kT * 16);
         }
     };
     // phase n issues: j0 B1 of t+1, j1 A1 of t+1, j2 A0 of t+2, j3 B0 of t+2 (t = n >> 2)
@@ -204,6 +238,22 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
                     c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][kk], bf[j][kk], c[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
+    // fp8 lo pass: the same fragment reads; a lane's two 16-B reads (kk = 0, 1) are one
+    // 32-B operand (A and B alike)
+    auto cat8 = [](const h8v& x, const h8v& y) {
+        const i4v u = __builtin_bit_cast(i4v, x), v = __builtin_bit_cast(i4v, y);
+        return __builtin_shufflevector(u, v, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    auto mma8 = [&](f4v (&c)[4][2], h8v (&bf)[2][2]) {  // one 128-deep fp8 K step
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                c[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(af[i][0], af[i][1]), cat8(bf[j][0], bf[j][1]),
+                                                                          c[i][j], 0, 0, 0, sc, 1, sc);
+        __builtin_amdgcn_s_setprio(0);
+    };
     auto sync_reads = [&](int n) {  // DMA counted, then the barrier; LDS reads retire behind it
 #if LLMI_G3_LGKM_EARLY
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -221,7 +271,8 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
     bar();
     if (wr == 1) bar();  // ping-pong: group 1 one barrier behind
 
-    for (int kt = 0; kt < KT; ++kt) {
+    auto ktile = [&](int kt, auto f8) {
+        constexpr bool F8 = decltype(f8)::value;
         const char* buf = lds + (kt & 1) * kBuf;
         const int n = 4 * kt;
         // j0: quadrant (A0, B0)
@@ -229,26 +280,29 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
         read_b(buf + 2 * kHalf, b0);
         issue(kt + 1, 3);
         sync_reads(n);
-        mma(acc[0][0], b0);
+        if constexpr (F8) mma8(acc[0][0], b0); else mma(acc[0][0], b0);
         bar();
         // j1: quadrant (A0, B1)
         read_b(buf + 3 * kHalf, b1);
         issue(kt + 1, 1);
         sync_reads(n + 1);
-        mma(acc[0][1], b1);
+        if constexpr (F8) mma8(acc[0][1], b1); else mma(acc[0][1], b1);
         bar();
         // j2: quadrant (A1, B1)
         read_a(buf + kHalf);
         issue(kt + 2, 0);
         sync_reads(n + 2);
-        mma(acc[1][1], b1);
+        if constexpr (F8) mma8(acc[1][1], b1); else mma(acc[1][1], b1);
         bar();
         // j3: quadrant (A1, B0)
         issue(kt + 2, 2);
         sync_reads(n + 3);
-        mma(acc[1][0], b0);
+        if constexpr (F8) mma8(acc[1][0], b0); else mma(acc[1][0], b0);
         bar();
-    }
+    };
+    const int KTh = lo8 ? KTs : KT;  // fp16 K tiles (then the fp8 lo tiles)
+    for (int kt = 0; kt < KTh; ++kt) ktile(kt, std::false_type{});
+    for (int kt = KTh; kt < KT; ++kt) ktile(kt, std::true_type{});
     if (wr == 0) bar();  // equal barrier counts
 
 #if LLMI_G3_EXP == 4
@@ -285,6 +339,13 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
             const int m = m0 + row;
             if (m >= a.m) continue;
             const h8v v = *reinterpret_cast<const h8v*>(img + (pl * kTile + row) * kEpiRowB + ch * 16);
+            if (pl && lo8) {  // e4m3 bytes [m, ldy] of the lo plane
+                uint2 q;
+                q.x = lo8_pack4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+                q.y = lo8_pack4((float)v[4], (float)v[5], (float)v[6], (float)v[7]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<char*>(a.y_lo + (size_t)m * a.ldy) + ct * 128 + ch * 8) = q;
+                continue;
+            }
             _Float16* dst = (pl ? a.y_lo : a.y_hi) + (size_t)m * a.ldy + ct * 128 + ch * 8;
             *reinterpret_cast<h8v*>(dst) = v;
         }
@@ -340,7 +401,61 @@ int launch_g3(const Gemm2Args& a, int grid, hipStream_t s) {
     return LLMI_OK;
 }
 
+__global__ void w8_amax_kernel(const __half* w, size_t n, unsigned* amax) {
+    float m = 0.f;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(__half2float(w[i])));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));  // non-negative floats order as uints
+}
+// row r of the fp16 [rows, cols] weight -> the first cols bytes of e4m3 row r (stride 2 cols bytes)
+__global__ void w8_convert_kernel(const __half* w, size_t n8, int cols8, float scale, uint2* out) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 u = reinterpret_cast<const uint4*>(w)[i];
+        const __half2* h = reinterpret_cast<const __half2*>(&u);
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float2 p = __half22float2(h[j]);
+            f[2 * j] = fminf(fmaxf(p.x * scale, -448.f), 448.f);
+            f[2 * j + 1] = fminf(fmaxf(p.y * scale, -448.f), 448.f);
+        }
+        uint2 q;
+        q.x = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false), true);
+        q.y = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false), true);
+        out[i + (i / cols8) * cols8] = q;
+    }
+}
+
 }  // namespace
+
+int w8_prepare(const void* w16, int rows, int cols, void* w8, int* exp_out, hipStream_t s) {
+    const size_t count = (size_t)rows * cols;
+    LLMI_REQUIRE(w16 && w8 && exp_out && rows > 0 && cols > 0 && cols % 8 == 0 &&
+                     (reinterpret_cast<uintptr_t>(w16) & 15) == 0 && (reinterpret_cast<uintptr_t>(w8) & 15) == 0,
+                 "w8_prepare: bad arguments");
+    unsigned* d = nullptr;
+    LLMI_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(unsigned), s));
+    LLMI_HIP(hipMemsetAsync(d, 0, sizeof(unsigned), s));
+    hipLaunchKernelGGL(w8_amax_kernel, dim3(1024), dim3(256), 0, s, static_cast<const __half*>(w16), count, d);
+    unsigned bits = 0;
+    LLMI_HIP(hipMemcpyAsync(&bits, d, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    LLMI_HIP(hipStreamSynchronize(s));
+    LLMI_HIP(hipFreeAsync(d, s));
+    float amax;
+    memcpy(&amax, &bits, 4);
+    int e = 0;
+    if (amax > 0.f && std::isfinite(amax)) {
+        e = (int)std::floor(std::log2(448.0 / (double)amax));
+        while (std::ldexp((double)amax, e) > 448.0) --e;
+        e = std::max(-100, std::min(100, e));
+    }
+    hipLaunchKernelGGL(w8_convert_kernel, dim3(2048), dim3(256), 0, s, static_cast<const __half*>(w16), count / 8, cols / 8,
+                       (float)std::ldexp(1.0, e), static_cast<uint2*>(w8));
+    LLMI_HIP(hipGetLastError());
+    *exp_out = e;
+    return LLMI_OK;
+}
 
 bool gemm3_supported(int n, int k, int epi, int ksplit) {
     const int ncols = (epi == EPI_SILU_MUL) ? n / 2 : n;
@@ -356,6 +471,8 @@ int gemm3_launch(Gemm2Args a, hipStream_t s) {
     LLMI_REQUIRE(gemm3_supported(a.n, a.k, a.epi, a.ksplit),
                  "gemm3: N a multiple of 256 (gate_up: 2 x 128), K a multiple of 64, >= 2 K tiles of 64 per slice");
     LLMI_REQUIRE(a.w_kblock == 0, "gemm3: head-major W blocks are not supported");
+    LLMI_REQUIRE((uint64_t)a.n * a.k * 2 < (1ull << 32) && (uint64_t)a.m * a.lda * 2 < (1ull << 32),
+                 "gemm3: W and A planes must each be under 4 GiB (32-bit DMA offsets)");
     LLMI_REQUIRE(a.epi == EPI_SILU_MUL ? (a.y || a.y_hi) : (a.epi == EPI_SLAB ? a.slab != nullptr : a.y != nullptr),
                  "gemm3: null output");
     LLMI_REQUIRE(a.lda % 8 == 0 && (reinterpret_cast<uintptr_t>(a.a[0]) & 15) == 0 &&
@@ -367,6 +484,11 @@ int gemm3_launch(Gemm2Args a, hipStream_t s) {
                      (a.ldy % 8 == 0 && (reinterpret_cast<uintptr_t>(a.y_hi) & 15) == 0 &&
                       (!a.y_lo || (reinterpret_cast<uintptr_t>(a.y_lo) & 15) == 0)),
                  "gemm3: fp16 output planes must be 16-B aligned with ldy % 8 == 0");
+    LLMI_REQUIRE(!a.lo8 || (a.planes == 2 && a.w8 && a.k % (2 * kK) == 0 && a.k / (2 * kK) >= a.ksplit &&
+                            (reinterpret_cast<uintptr_t>(a.w8) & 15) == 0 &&
+                            (a.epi != EPI_SILU_MUL || (a.y_hi && a.y_lo))),
+                 "gemm3: the fp8 lo plane needs planes = 2, w8, K a multiple of 128, >= one 128-deep tile per slice "
+                 "and (gate_up) both output planes");
     const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
     a.n_tiles = ncols / ((a.epi == EPI_SILU_MUL) ? 128 : kTile);
     const int grid = ((a.m + kTile - 1) / kTile) * a.n_tiles * a.ksplit;

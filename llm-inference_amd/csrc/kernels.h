@@ -96,7 +96,17 @@ struct Gemm2Args {
     int ksplit = 1;                // EPI_SLAB: K slices (K / ksplit a multiple of 64, and of w_kblock)
     float* slab = nullptr;         // EPI_SLAB: [ksplit][m][ldy] partial sums
     int n_tiles = 0;               // set by gemm2_launch
+    // gemm3 only, planes = 2: the lo plane a[1] is e4m3 of lo * 2^kLo8Exp (common.h) in
+    // the first lda bytes of each 2 lda-byte row, against w8 = e4m3(W * 2^w8_exp) (rows of
+    // 2 k bytes, the first k used; w8_prepare) on the block-scaled fp8 MFMA; EPI_SILU_MUL
+    // then writes y_lo in the same byte format (K a multiple of 128)
+    int lo8 = 0;
+    const void* w8 = nullptr;
+    int w8_exp = 0;
 };
+// e4m3(W * 2^exp) of an fp16 [rows, cols] weight (exp chosen so that max |W| * 2^exp <= 448),
+// rows of 2 cols bytes with the first cols used (the fp16 row stride, gemm3.hip); synchronises s
+int w8_prepare(const void* w16, int rows, int cols, void* w8, int* exp_out, hipStream_t s);
 bool gemm2_supported(int n, int k, int epi);
 int gemm2_launch(Gemm2Args a, hipStream_t s);
 // the same GEMM on 256 x 256 tiles with a ping-pong 8-wave schedule (gemm3.hip)
@@ -109,7 +119,8 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
 // rows of x (+= the ksplit slices of slab, in slice order, written back to x),
 // then optional RMSNorm, then fp16 planes hi[, lo] (hi null: the combine alone)
 int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,
-                      _Float16* lo, int ldh, hipStream_t s, const float* slab = nullptr, int ksplit = 0);
+                      _Float16* lo, int ldh, hipStream_t s, const float* slab = nullptr, int ksplit = 0,
+                      bool lo8 = false);  // lo8: e4m3 lo bytes in the first ldh bytes of each row (common.h lo8_pack4)
 
 // ------------------------------------------------- prefill attention
 // rope + KV-cache write of M rows, then causal attention over cache slots
@@ -130,6 +141,7 @@ struct PrefillAttnArgs {
     int mfma_planes = 0;
     _Float16* out_hi = nullptr;
     _Float16* out_lo = nullptr;
+    int out_lo8 = 0;               // out_lo rows hold e4m3 bytes in their first half (common.h lo8_pack4)
     // MFMA form: scratch for the split-key partials (null: one workgroup per query block)
     float* split_ws = nullptr;
     size_t split_ws_floats = 0;

@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
                                                                      int heads, int kv_heads, const __half* k_cache,
                                                                      const __half* v_cache, int max_seq, float* out,
                                                                      _Float16* out_hi, _Float16* out_lo, int ldo,
-                                                                     int cb, float* ws, int maxc) {
+                                                                     int cb, float* ws, int maxc, int lo8) {
     __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 + D * KB * 2 + 4 * P * 16 * KB * 2];
     char* Ks = smem;                 // [key][256 B], chunk ^= key & 15
     char* Vt = smem + KB * D * 2;    // [dim][128 B], chunk ^= vswz(dim)
@@ -491,7 +491,12 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
                 lv[e] = (_Float16)(v[e] - (float)hv[e]);
             }
             *reinterpret_cast<h8*>(out_hi + idx) = hv;
-            if (out_lo) *reinterpret_cast<h8*>(out_lo + idx) = lv;
+            if (out_lo && lo8)
+                *reinterpret_cast<uint2*>(reinterpret_cast<char*>(out_lo + (size_t)row * ldo) + (size_t)h * D + 8 * c8) =
+                    make_uint2(lo8_pack4(v[0] - (float)hv[0], v[1] - (float)hv[1], v[2] - (float)hv[2], v[3] - (float)hv[3]),
+                               lo8_pack4(v[4] - (float)hv[4], v[5] - (float)hv[5], v[6] - (float)hv[6], v[7] - (float)hv[7]));
+            else if (out_lo)
+                *reinterpret_cast<h8*>(out_lo + idx) = lv;
         } else {
             *reinterpret_cast<float4*>(out + idx) = x0;
             *reinterpret_cast<float4*>(out + idx + 4) = x1;
@@ -507,7 +512,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
 template <int MAXC>
 __global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const float* ws, int maxc, int cb, int m_rows,
                                                                       int p0, float* out, _Float16* out_hi,
-                                                                      _Float16* out_lo, int ldo) {
+                                                                      _Float16* out_lo, int ldo, int lo8) {
     const int qb = blockIdx.x, h = blockIdx.y, nqb = gridDim.x;
     const int nch = (pf_nkb(qb, p0, m_rows) + cb - 1) / cb;
     if (nch <= 1) return;  // written directly by the attention kernel
@@ -547,14 +552,20 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const floa
         const size_t idx = (size_t)row * ldo + (size_t)h * D + d0;
         if (out_hi) {
             h8 hv, lv;
+            float r[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const float v = acc[i] * inv;
                 hv[i] = (_Float16)v;
-                lv[i] = (_Float16)(v - (float)hv[i]);
+                r[i] = v - (float)hv[i];
+                lv[i] = (_Float16)r[i];
             }
             *reinterpret_cast<h8*>(out_hi + idx) = hv;
-            if (out_lo) *reinterpret_cast<h8*>(out_lo + idx) = lv;
+            if (out_lo && lo8)
+                *reinterpret_cast<uint2*>(reinterpret_cast<char*>(out_lo + (size_t)row * ldo) + (size_t)h * D + d0) =
+                    make_uint2(lo8_pack4(r[0], r[1], r[2], r[3]), lo8_pack4(r[4], r[5], r[6], r[7]));
+            else if (out_lo)
+                *reinterpret_cast<h8*>(out_lo + idx) = lv;
         } else {
             *reinterpret_cast<float4*>(out + idx) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
             *reinterpret_cast<float4*>(out + idx + 4) = make_float4(acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv);
@@ -614,15 +625,15 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
             if (a.mfma_planes == 2)
                 hipLaunchKernelGGL(attn_prefill_mfma_kernel<2>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
                                    a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
-                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc);
+                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc, a.out_lo8);
             else
                 hipLaunchKernelGGL(attn_prefill_mfma_kernel<1>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
                                    a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
-                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc);
+                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc, a.out_lo8);
             if (maxc > 1) {
 #define PF_MERGE(C)                                                                                              \
     hipLaunchKernelGGL(attn_prefill_merge_kernel<C>, dim3(nqb, a.heads), dim3(kThreads), 0, s, a.split_ws, maxc, cb, \
-                       a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D)
+                       a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D, a.out_lo8)
                 if (maxc <= 2)
                     PF_MERGE(2);
                 else if (maxc <= 4)

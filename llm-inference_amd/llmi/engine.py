@@ -85,8 +85,13 @@ class Engine:
     def decode(self, n_steps: int, use_graph: bool = True):
         call("llmi_engine_decode", self._h, n_steps, 1 if use_graph else 0)
 
-    def prefill(self, n_tokens: int, exact: bool = True):
-        call("llmi_engine_prefill", self._h, n_tokens, 1 if exact else 0)
+    def prefill(self, n_tokens: int, exact=True):
+        """exact: True / 1 fp32-faithful (two fp16 planes), 2 fp16 hi + e4m3 lo planes on
+        the fp8 MFMA (~1e-4), False / 0 fp16 activations (llmi_engine_prefill)."""
+        mode = int(exact)
+        if mode not in (0, 1, 2):
+            raise ValueError("prefill: exact must be False/0, True/1 or 2")
+        call("llmi_engine_prefill", self._h, n_tokens, mode)
 
     def sync(self):
         call("llmi_engine_sync", self._h)

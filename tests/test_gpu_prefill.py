@@ -113,6 +113,45 @@ def test_prefill_fast_mode_f6():
     assert r < 5e-3
 
 
+def test_prefill_fp8_lo_mode_f6():
+    """exact=2: fp16 hi planes + e4m3 lo planes on the block-scaled fp8 MFMA (gemm3 lo8):
+    inside the 1e-3 bar, within 10 % of the exact planes' error (with the fp16 cache both
+    sit at the cache's rounding, ~1e-4) and below the fp16-activation mode's."""
+    f = np.load(os.path.join(G, "f6_prefill.npz"))
+    cfg = preset("llama2-7b", layers=1, max_seq=520)
+    rs = {}
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        for mode in (2, 0, 1):
+            e.set_prompt(f["ids"])
+            e.prefill(len(f["ids"]), exact=mode)
+            rs[mode] = rel(e.logits(), f["last_logits"])
+            if mode == 2:
+                toks = e.tokens()
+    print("f6 prefill logits rel-L2 vs reference, fp8-lo / fp16-activation / exact: "
+          f"{rs[2]:.3e} / {rs[0]:.3e} / {rs[1]:.3e}")
+    assert rs[2] < LOGIT_TOL
+    assert rs[2] < 1.1 * rs[1] and rs[2] < rs[0]
+    np.testing.assert_array_equal(toks[:512], f["ids"])
+    assert toks[512] == int(np.argmax(f["last_logits"]))
+
+
+def test_prefill_fp8_lo_mode_falls_back_with_fp32_cache():
+    """The fp8 lo pass needs the fp16-cache MFMA attention; with an fp32 cache exact=2
+    runs the exact planes (bitwise the exact=1 result)."""
+    cfg = preset("tiny", max_seq=64)
+    cfg.kv_dtype = _lib.F32
+    prompt = synth_prompt(3, 40, cfg.vocab)
+    out = {}
+    with Engine(cfg) as e:
+        e.load_synthetic(2)
+        for mode in (1, 2):
+            e.set_prompt(prompt)
+            e.prefill(len(prompt), exact=mode)
+            out[mode] = e.logits().copy()
+    np.testing.assert_array_equal(out[1], out[2])
+
+
 @pytest.mark.parametrize("name,cfgname,over,wdt", [
     ("tiny.npz", "tiny", {}, _lib.F16),
     ("f3_decode.npz", "llama2-7b", dict(layers=2, max_seq=64), _lib.F16),
@@ -157,19 +196,21 @@ def test_prefill_partial_and_chunked_equals_decode_path():
     assert r < LOGIT_TOL
 
 
-def test_full_7b_prefill_512_matches_decode_path():
-    """Config 3: Llama-2-7B (32 layers, fp16 weights + KV), 512-row prompt."""
+@pytest.mark.parametrize("exact", [1, 2])
+def test_full_7b_prefill_512_matches_decode_path(exact):
+    """Config 3: Llama-2-7B (32 layers, fp16 weights + KV), 512-row prompt; exact = 2
+    is the fp8-lo-plane mode."""
     cfg = preset("llama2-7b", max_seq=640)
     prompt = synth_prompt(1, 512, cfg.vocab)
     with Engine(cfg) as e:
         e.load_synthetic(0)
         ref_toks = e.generate(prompt, 16)
         ref_logits = e.logits()
-        toks = e.generate(prompt, 16, prefill=True)
+        toks = e.generate(prompt, 16, prefill=True, exact=exact)
         logits = e.logits()
     np.testing.assert_array_equal(toks, ref_toks)
     r = rel(logits, ref_logits)
-    print(f"full 7B prefill-512 + 15 decode vs decode path logits rel-L2: {r:.3e}")
+    print(f"full 7B prefill-512 (exact={exact}) + 15 decode vs decode path logits rel-L2: {r:.3e}")
     assert r < LOGIT_TOL
 
 

@@ -32,6 +32,24 @@ __global__ void fill_kernel(_Float16* p, size_t n, unsigned seed, float scale) {
     }
 }
 
+// exact-data mode: integers j / den with |j| <= 15 (e4m3-exact once scaled by a power of two)
+__global__ void fill_int_kernel(_Float16* p, size_t n, unsigned seed, float den) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u ^ seed;
+        x ^= x >> 15; x *= 2246822519u; x ^= x >> 13;
+        p[i] = (_Float16)((float)((int)(x % 31u) - 15) / den);
+    }
+}
+// the lo8 plane of gemm3 from fp16 lo values: e4m3(lo * 2^12) in the first lda bytes of each 2 lda-byte row
+__global__ void lo8_kernel(const _Float16* lo, size_t rows, int lda, unsigned char* out) {
+    const size_t n4 = rows * lda / 4;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t e = 4 * i, r = e / lda, c = e % lda;
+        *reinterpret_cast<uint32_t*>(out + r * 2 * lda + c) =
+            lo8_pack4((float)lo[e], (float)lo[e + 1], (float)lo[e + 2], (float)lo[e + 3]);
+    }
+}
+
 static void fill(_Float16* p, size_t n, unsigned seed, float scale) {
     hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, 0, p, n, seed, scale);
     CK(hipGetLastError());
@@ -64,7 +82,8 @@ int main(int argc, char** argv) {
     const int iters = argc > 2 ? std::atoi(argv[2]) : 20;
     const int check = argc > 3 ? std::atoi(argv[3]) : 1;
     const std::string only = argc > 4 ? argv[4] : "";  // run only this shape (and planes = argv[5])
-    const int only_planes = argc > 5 ? std::atoi(argv[5]) : 0;
+    const int only_planes = argc > 5 ? std::atoi(argv[5]) : 0;  // 3 = the fp8 lo plane (lo8)
+    const int exact_data = argc > 6 ? std::atoi(argv[6]) : 0;   // 1: e4m3-exact lo and W (checks the fp8 k map)
     std::vector<Shape> shapes = {
         {"qkv", 12288, 4096, EPI_STORE, 1},   {"qkv_s2", 12288, 4096, EPI_SLAB, 2},
         {"o_s2", 4096, 4096, EPI_SLAB, 2},    {"o_s4", 4096, 4096, EPI_SLAB, 4},
@@ -80,26 +99,41 @@ int main(int argc, char** argv) {
         maxW = std::max(maxW, (size_t)s.n * s.k);
         maxY = std::max(maxY, (size_t)m * s.n * (s.epi == EPI_SLAB ? s.ksplit : 1));
     }
-    _Float16 *ah, *al, *w, *yh, *yl;
+    _Float16 *ah, *al, *al8, *w, *w8, *yh, *yl;
     float *y2, *y3, *slab;
     CK(hipMalloc(&ah, maxA * 2));
     CK(hipMalloc(&al, maxA * 2));
     CK(hipMalloc(&w, maxW * 2));
+    CK(hipMalloc(&al8, maxA * 2));
+    CK(hipMalloc(&w8, maxW * 2));
     CK(hipMalloc(&y2, maxY * 4));
     CK(hipMalloc(&y3, maxY * 4));
     CK(hipMalloc(&slab, maxY * 4));
     CK(hipMalloc(&yh, maxY * 2));
     CK(hipMalloc(&yl, maxY * 2));
-    fill(ah, maxA, 1, 1.0f);
-    fill(al, maxA, 2, 1.0f / 2048);
-    fill(w, maxW, 3, 0.05f);
+    if (exact_data) {  // hi = 0, lo = j / 4096, W = j / 64: the lo8 pass is then exact (fp32 sums of integers)
+        CK(hipMemset(ah, 0, maxA * 2));
+        hipLaunchKernelGGL(fill_int_kernel, dim3(2048), dim3(256), 0, 0, al, maxA, 2u, 4096.f);
+        hipLaunchKernelGGL(fill_int_kernel, dim3(2048), dim3(256), 0, 0, w, maxW, 3u, 64.f);
+    } else {
+        fill(ah, maxA, 1, 1.0f);
+        fill(al, maxA, 2, 1.0f / 2048);
+        fill(w, maxW, 3, 0.05f);
+    }
     CK(hipDeviceSynchronize());
 
     for (auto& s : shapes) {
         if (!only.empty() && only != s.name) continue;
         const int m = std::string(s.name) == "sq4096" ? 4096 : M;
-        for (int planes = 1; planes <= 2; ++planes) {
-            if (only_planes && planes != only_planes) continue;
+        int w8e = 0;
+        if (only_planes == 0 || only_planes == 3) {
+            if (w8_prepare(w, s.n, s.k, w8, &w8e, 0) != 0) return 1;
+            hipLaunchKernelGGL(lo8_kernel, dim3(2048), dim3(256), 0, 0, al, (size_t)m, s.k, (unsigned char*)al8);
+            CK(hipDeviceSynchronize());
+        }
+        for (int pm = 1; pm <= 3; ++pm) {
+            if (only_planes && pm != only_planes) continue;
+            const int planes = pm == 3 ? 2 : pm;
             Gemm2Args g;
             g.a[0] = ah; g.a[1] = al; g.planes = planes; g.lda = s.k; g.w = w; g.m = m; g.n = s.n; g.k = s.k;
             g.epi = s.epi; g.ksplit = s.ksplit; g.slab = slab; g.ldy = s.epi == EPI_SILU_MUL ? s.n / 2 : s.n;
@@ -109,6 +143,66 @@ int main(int argc, char** argv) {
             g.y = y2;
             const double flop = 2.0 * m * s.n * s.k * planes;
             float us2 = -1.f;
+            Gemm2Args g8 = g;  // the lo8 form of g (gemm3 only)
+            g8.a[1] = al8; g8.lo8 = 1; g8.w8 = w8; g8.w8_exp = w8e;
+            if (pm == 3) {
+                float us3 = -1.f;
+                if (gemm3_supported(s.n, s.k, s.epi, s.ksplit) && s.k % 128 == 0 && s.k / 128 >= s.ksplit)
+                    us3 = time_us([&] { gemm3_launch(g8, 0); }, iters);
+                double err = -1;
+                if (check && us3 > 0) {  // vs gemm2 with both fp16 planes (EPI_STORE; SILU: fp32 output)
+                    Gemm2Args c = g;
+                    c.epi = s.epi == EPI_SLAB ? EPI_STORE : s.epi;
+                    c.y_hi = c.y_lo = nullptr;
+                    c.y = y2;
+                    gemm2_launch(c, 0);
+                    const size_t ny = (size_t)m * g.ldy;
+                    std::vector<float> h2(ny), h3(ny, 0.f);
+                    CK(hipDeviceSynchronize());
+                    CK(hipMemcpy(h2.data(), y2, ny * 4, hipMemcpyDeviceToHost));
+                    if (s.epi == EPI_SLAB) {
+                        gemm3_launch(g8, 0);
+                        CK(hipDeviceSynchronize());
+                        std::vector<float> sl(ny * s.ksplit);
+                        CK(hipMemcpy(sl.data(), slab, sl.size() * 4, hipMemcpyDeviceToHost));
+                        for (int q = 0; q < s.ksplit; ++q)
+                            for (size_t i = 0; i < ny; ++i) h3[i] += sl[q * ny + i];
+                    } else if (s.epi == EPI_SILU_MUL) {  // hi plane + the e4m3 lo plane back to fp32
+                        gemm3_launch(g8, 0);
+                        CK(hipDeviceSynchronize());
+                        std::vector<_Float16> hh(ny);
+                        std::vector<unsigned char> ll(ny * 2);
+                        CK(hipMemcpy(hh.data(), yh, ny * 2, hipMemcpyDeviceToHost));
+                        CK(hipMemcpy(ll.data(), yl, ny * 2, hipMemcpyDeviceToHost));
+                        auto e4m3 = [](unsigned char b) {
+                            const int sg = b >> 7, ex = (b >> 3) & 15, mn = b & 7;
+                            const double v = ex ? std::ldexp(1.0 + mn / 8.0, ex - 7) : std::ldexp(mn / 8.0, -6);
+                            return sg ? -v : v;
+                        };
+                        for (size_t i = 0; i < ny; ++i) {
+                            const size_t r = i / g.ldy, cc = i % g.ldy;
+                            h3[i] = (float)((double)hh[i] + std::ldexp(e4m3(ll[r * 2 * g.ldy + cc]), -12));
+                        }
+                    } else {
+                        Gemm2Args c3 = g8;
+                        c3.y = y3;
+                        gemm3_launch(c3, 0);
+                        CK(hipDeviceSynchronize());
+                        CK(hipMemcpy(h3.data(), y3, ny * 4, hipMemcpyDeviceToHost));
+                    }
+                    double mx = 0, ref = 0;
+                    for (size_t i = 0; i < ny; ++i) {
+                        mx = std::max(mx, (double)std::fabs(h2[i] - h3[i]));
+                        ref = std::max(ref, (double)std::fabs(h2[i]));
+                    }
+                    err = mx / (ref > 0 ? ref : 1);
+                }
+                std::printf("{\"shape\": \"%s\", \"m\": %d, \"n\": %d, \"k\": %d, \"planes\": \"hi+lo8\", \"ksplit\": %d, "
+                            "\"w8_exp\": %d, \"exact_data\": %d, \"gemm3_us\": %.2f, \"rel_err\": %.3g}\n",
+                            s.name, m, s.n, s.k, s.ksplit, w8e, exact_data, us3, err);
+                std::fflush(stdout);
+                continue;
+            }
             if (gemm2_supported(s.n, s.k, s.epi) && (s.epi != EPI_SLAB || s.k % (s.ksplit * 64) == 0) && s.ksplit <= 8)
                 us2 = time_us([&] { gemm2_launch(g, 0); }, iters);
             float us3 = -1.f;

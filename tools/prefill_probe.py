@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the batched prefill (config 3: Llama-2-7B, 512 prompt rows) on one GPU,
 both GEMM precisions, and print JSON (ms, TFLOP/s on the algorithmic FLOPs).
-    python tools/prefill_probe.py [rows] [iters] [exact|fast]"""
+    python tools/prefill_probe.py [rows] [iters] [exact|exact8|fast]"""
 import json
 import os
 import sys
@@ -23,7 +23,7 @@ def prefill_flops(cfg, m):
 def main():
     m = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    modes = {"exact": (True,), "fast": (False,)}.get(sys.argv[3] if len(sys.argv) > 3 else "", (True, False))
+    modes = {"exact": (1,), "exact8": (2,), "fast": (0,)}.get(sys.argv[3] if len(sys.argv) > 3 else "", (1, 2, 0))
     cfg = preset("llama2-7b", max_seq=m + 64)
     prompt = synth_prompt(1, m, cfg.vocab)
     out = {"m": m, "flops": prefill_flops(cfg, m)}
@@ -39,7 +39,7 @@ def main():
                 e.sync()
                 ts.append(time.perf_counter() - t0)
             ms = 1e3 * min(ts[1:])
-            key = "exact" if exact else "fast"
+            key = {1: "exact", 2: "exact8", 0: "fast"}[exact]
             out[key] = {"ms": ms, "tflops": out["flops"] / (ms * 1e-3) / 1e12, "token": int(e.tokens()[m])}
     print(json.dumps(out))
 
