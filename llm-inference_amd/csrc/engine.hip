@@ -164,6 +164,10 @@ struct Engine {
     };
     std::vector<W8Layer> w8l;
     char* w8blob = nullptr;
+    // split mode 3's gate_up on every CU (gemm3_silu_bal_kernel): lo partial slots + flags
+    float* pf_bal = nullptr;
+    unsigned* pf_bal_flags = nullptr;
+    int n_cu = 0;
     int host_next_pos = 0, prompt_len = 0;
     unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
     // llmi_engine_debug_timeline: every stamped launch of a recorded step gets its own
@@ -197,6 +201,8 @@ struct Engine {
         if (scratch) (void)hipFree(scratch);
         if (pf) (void)hipFree(pf);
         if (w8blob) (void)hipFree(w8blob);
+        if (pf_bal) (void)hipFree(pf_bal);
+        if (pf_bal_flags) (void)hipFree(pf_bal_flags);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
@@ -861,9 +867,20 @@ struct Engine {
             LLMI_TRY(w8_prepare(layers[l].gu, 2 * il, H, w.gu, &w.gu_e, stream));
             LLMI_TRY(w8_prepare(layers[l].down, H, il, w.down, &w.down_e, stream));
         }
+        if (!pf_bal) {
+            const size_t sb = gemm3_bal_slab_bytes(pf_rows, 2 * il);
+            LLMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+            if (sb > 0) {
+                const size_t nflags = sb / (kBalTileBytes / 2);  // two per tile
+                LLMI_HIP(hipMalloc(&pf_bal, sb));
+                LLMI_HIP(hipMalloc(&pf_bal_flags, nflags * sizeof(unsigned)));
+                LLMI_HIP(hipMemsetAsync(pf_bal_flags, 0, nflags * sizeof(unsigned), stream));
+            }
+        }
         LLMI_HIP(hipStreamSynchronize(stream));
         return LLMI_OK;
     }
+    static constexpr size_t kBalTileBytes = (size_t)2 * 256 * 256 * 4;  // two fp32 256 x 256 slots
 
     // One prefill layer on the LDS-DMA GEMM (gemm2.hip): RMSNorm + split into fp16
     // planes, q/k/v GEMM, rope + KV write + causal attention, split, o_proj (+residual),
@@ -925,11 +942,15 @@ struct Engine {
         // (o slices into x) + rmsnorm + gate_up + silu * up -> planes of the down GEMM's input
         LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.ffn_norm, edt, c.rms_eps, pf_ah, lo, H, stream, pf_slab, so, f8));
         g.lda = H; g.w = L.gu; g.n = 2 * il; g.k = H;
-        if (f8) { g.w8 = W8->gu; g.w8_exp = W8->gu_e; }
+        if (f8) {  // + the lo pass spread over the CUs its 256 x 256 tiles leave idle
+            g.w8 = W8->gu; g.w8_exp = W8->gu_e;
+            g.bal_slab = pf_bal; g.bal_flags = pf_bal_flags; g.bal_grid = n_cu; g.err = &st->error;
+        }
         g.epi = EPI_SILU_MUL; g.pair_off = il; g.y = nullptr; g.y_hi = pf_act_h(); g.y_lo = split >= 2 ? pf_act_l() : nullptr;
         g.ldy = il;
         LLMI_TRY(gemm3_supported(g.n, H, EPI_SILU_MUL, 1) ? gemm3_launch(g, stream) : gemm2_launch(g, stream));
         // down + residual: K slices into slabs (gemm3: 8 uneven slices, 256 workgroups)
+        g.bal_slab = nullptr; g.bal_flags = nullptr;
         g.a[0] = pf_act_h(); g.a[1] = split >= 2 ? pf_act_l() : nullptr;
         g.lda = il; g.w = L.down; g.n = H; g.k = il;
         if (f8) { g.w8 = W8->down; g.w8_exp = W8->down_e; }
@@ -1039,7 +1060,8 @@ struct Engine {
         DecodeState h;
         LLMI_HIP(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
         LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error) +
-                                       " (1: token id out of range, 2: position overflow, 4: attention split count != device position)");
+                                       " (1: token id out of range, 2: position overflow, 4: attention split count != device position, "
+                                       "16: a prefill gate_up lo partial never arrived)");
         const int m = n < valid ? n : valid;
         if (m > 0) LLMI_HIP(hipMemcpy(out, tokens, (size_t)m * 4, hipMemcpyDeviceToHost));
         if (n_valid) *n_valid = valid;

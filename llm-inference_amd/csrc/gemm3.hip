@@ -44,6 +44,8 @@
 // At twice the fp16 MFMA rate and half the K tiles, the lo pass costs half of the
 // fp16 one; |lo| <= 2^-11 |a| and e4m3's 2^-4 steps leave ~2^-15 of |a W| per product.
 // Roofline: MFMA (fp16 dense 2.5 PFLOP/s); FLOPs per launch 2 * M * N * K * planes.
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <type_traits>
 
@@ -119,30 +121,19 @@ __device__ __forceinline__ void bar() {
 
 __device__ __forceinline__ float silu3(float v) { return v / (1.0f + expf(-v)); }
 
+// One tile's K loop into acc: nhi 64-deep fp16 K tiles of the hi plane from tile hi0, then
+// nlo tiles of the lo plane from tile lo0 (fp16 plane: 64-deep tiles; lo8: 128-deep fp8
+// tiles; both 128 B per LDS row). nhi + nlo >= 2: the prologue's counted wait covers the
+// first two tiles. Every wave passes the same barriers, and every LDS read has retired on
+// return, so the caller may reuse the LDS.
 template <int EPI>
-__global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, int ct, int hi0, int nhi, int lo0,
+                                       int nlo, f4v (&acc)[2][2][4][2]) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wr = w >> 2, wc = w & 3;  // wr is also the ping-pong group
     const int fr = lane & 15, fq = lane >> 4;
-
-    // bijective XCD remap, then tile-major over split-K slices, row tiles fastest
-    // (the row tiles of one W stripe run together on one XCD: W read once into L2)
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int S = (EPI == EPI_SLAB) ? a.ksplit : 1;
-    const int tile = id / S, slice = id - tile * S;
-    const int m_tiles = (a.m + kTile - 1) / kTile;
-    const int rt = tile % m_tiles, ct = tile / m_tiles;
-    const int m0 = rt * kTile;
-    // slice s covers K tiles [s * KT_all / S, (s + 1) * KT_all / S) of each plane
-    // (lo8: on 128-deep boundaries, so the slice's fp8 lo tiles are whole)
     const bool lo8 = a.lo8 != 0;
-    const int KT_all = lo8 ? a.k / (2 * kK) : a.k / kK;
-    const int kt0 = (lo8 ? 2 : 1) * (slice * KT_all / S);
-    const int KTs = (lo8 ? 2 : 1) * ((slice + 1) * KT_all / S) - kt0;  // 64-deep K tiles per plane in this slice
-    const int KT = lo8 ? KTs + KTs / 2 : KTs * a.planes;                // virtual K tiles ([hi | lo])
+    const int KT = nhi + nlo;  // virtual K tiles ([hi | lo])
 
     // per-thread DMA sources: instruction i of a half-image fills half-local bytes
     // i * 8192 + 16 t, which hold logical byte swz3(.) of the image
@@ -177,11 +168,11 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
 #if LLMI_G3_EXP == 1
         if (v >= 2) return;
 #endif
-        const int plane = v >= KTs ? 1 : 0;
+        const int plane = v >= nhi ? 1 : 0;
         const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (v & 1) * kBuf + half * kHalf + w * 1024);
         // fp8 rows keep the fp16 rows' byte stride (the first half of each row is used),
         // so the per-thread offsets serve both passes -- no second set of registers
-        const unsigned k0b = (lo8 && plane) ? (unsigned)(kt0 / 2 + v - KTs) * 128u : (unsigned)(kt0 + v - plane * KTs) * kK * 2u;
+        const unsigned k0b = (unsigned)(plane ? lo0 + v - nhi : hi0 + v) * 128u;
         const char* base = half < 2 ? abase[plane] : (lo8 && plane) ? w8base : wbase;  // uniform
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -195,16 +186,6 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
         const int c = min(n, n_last) - (n - 4);
         return 2 * max(0, min(4, c));
     };
-
-    f4v acc[2][2][4][2];
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
     h8v af[4][2], b0[2][2], b1[2][2];
     auto read_a = [&](const char* img) {
@@ -300,14 +281,31 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
         if constexpr (F8) mma8(acc[1][0], b0); else mma(acc[1][0], b0);
         bar();
     };
-    const int KTh = lo8 ? KTs : KT;  // fp16 K tiles (then the fp8 lo tiles)
+    const int KTh = lo8 ? nhi : KT;  // fp16 K tiles (then the fp8 lo tiles)
     for (int kt = 0; kt < KTh; ++kt) ktile(kt, std::false_type{});
     for (int kt = KTh; kt < KT; ++kt) ktile(kt, std::true_type{});
     if (wr == 0) bar();  // equal barrier counts
+}
 
-#if LLMI_G3_EXP == 4
-    if (KT > 0) return;  // timing experiment: no epilogue stores
-#endif
+__device__ __forceinline__ void zero_acc(f4v (&acc)[2][2][4][2]) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+}
+
+// the tile's epilogue (slice: the EPI_SLAB K slice)
+template <int EPI>
+__device__ __forceinline__ void g3_epilogue(const Gemm2Args& a, char* lds, f4v (&acc)[2][2][4][2], int m0, int ct,
+                                            int slice) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w >> 2, wc = w & 3;
+    const int fr = lane & 15, fq = lane >> 4;
+    const bool lo8 = a.lo8 != 0;
     // epilogue: acc[qa][qb][i][j] register e is tile row qa*128 + wr*64 + 16 i + 4 fq + e,
     // tile column qb*128 + wc*32 + 16 j + fr (SILU: qb 0 gate, qb 1 its up column)
     if (EPI == EPI_SILU_MUL && a.y_hi) {
@@ -390,6 +388,150 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
 }
 
 template <int EPI>
+__global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    // bijective XCD remap, then tile-major over split-K slices, row tiles fastest
+    // (the row tiles of one W stripe run together on one XCD: W read once into L2)
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int S = (EPI == EPI_SLAB) ? a.ksplit : 1;
+    const int tile = id / S, slice = id - tile * S;
+    const int m_tiles = (a.m + kTile - 1) / kTile;
+    const int rt = tile % m_tiles, ct = tile / m_tiles;
+    const int m0 = rt * kTile;
+    // slice s covers K tiles [s * KT_all / S, (s + 1) * KT_all / S) of each plane
+    // (lo8: on 128-deep boundaries, so the slice's fp8 lo tiles are whole)
+    const bool lo8 = a.lo8 != 0;
+    const int KT_all = lo8 ? a.k / (2 * kK) : a.k / kK;
+    const int kt0 = (lo8 ? 2 : 1) * (slice * KT_all / S);
+    const int KTs = (lo8 ? 2 : 1) * ((slice + 1) * KT_all / S) - kt0;  // 64-deep K tiles per plane in this slice
+    f4v acc[2][2][4][2];
+    zero_acc(acc);
+    g3_run<EPI>(a, lds, m0, ct, kt0, KTs, lo8 ? kt0 / 2 : kt0, lo8 ? KTs / 2 : (a.planes == 2 ? KTs : 0), acc);
+#if LLMI_G3_EXP == 4
+    if (KTs > 0) return;  // timing experiment: no epilogue stores
+#endif
+    g3_epilogue<EPI>(a, lds, acc, m0, ct, slice);
+}
+
+// gate_up in the fp8-lo mode with every CU busy (gemm3_launch with bal_slab): its 172
+// 256 x 256 tiles alone leave 84 of 256 CUs idle for the whole launch. Workgroups
+// [0, n_lo) are lo workers: the fp8 lo pass of all tiles, in units of two 128-deep K tiles,
+// is split evenly over them (contiguous ranges that cross tile boundaries; a tile is
+// touched by at most two workers); each piece's fp32 partial goes to its tile's slot, then
+// a release fence and an epoch flag. Workgroups [n_lo, grid) own one tile each: its fp16
+// hi pass, then the tile's one or two lo partials (acquire; added in slot order, so the
+// result is repeatable), then the SiLU epilogue. Workers have the lower ids and are
+// dispatched first, so a waiting owner never holds a CU its producer needs; every wait is
+// bounded (2 s of s_memrealtime, then error bit 16 and the epilogue without that slot).
+__global__ __launch_bounds__(kT) void gemm3_silu_bal_kernel(Gemm2Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    WgStamp ts(a.stamps);  // [1] K loop(s) done, [2] partials in / published
+    const int t = threadIdx.x;
+    const int m_tiles = (a.m + kTile - 1) / kTile;
+    const int n_tiles = m_tiles * a.n_tiles;
+    const int n_lo = (int)gridDim.x - n_tiles;
+    // a tile's first `own` pairs of 128-deep lo tiles stay with its owner (balance: an fp8
+    // lo tile costs ~1.4 fp16 ones); the other P units go to the workers
+    const int own = a.bal_own;
+    const int P = a.k / 256 - own;
+    const int U = n_tiles * P;
+    auto worker_of = [&](int x) { return (int)(((long)(x + 1) * n_lo + U - 1) / U) - 1; };
+    auto slot_ptr = [&](int tile, int slot) {
+        return reinterpret_cast<float4*>(a.bal_slab) + (size_t)(tile * 2 + slot) * 32 * kT + t;
+    };
+    f4v acc[2][2][4][2];
+    const int bid = blockIdx.x;
+    if (bid < n_lo) {
+        const int u1 = (int)((long)(bid + 1) * U / n_lo);
+        for (int u = (int)((long)bid * U / n_lo); u < u1;) {
+            const int tile = u / P, ue = min(u1, (tile + 1) * P);
+            const int slot = bid == worker_of(tile * P) ? 0 : 1;
+            zero_acc(acc);
+            g3_run<EPI_SILU_MUL>(a, lds, (tile % m_tiles) * kTile, tile / m_tiles, 0, 0, 2 * (own + u - tile * P),
+                                 2 * (ue - u), acc);
+            float4* dst = slot_ptr(tile, slot);
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const f4v v = acc[x][y][i][j];
+                            dst[(size_t)(((x * 2 + y) * 4 + i) * 2 + j) * kT] = make_float4(v[0], v[1], v[2], v[3]);
+                        }
+            // every wave's stores complete, then ONE release (one L2 write-back per piece: a
+            // fence in each of the 8 waves wrote the XCD's L2 back 8 times and slowed the
+            // owners beside it), then the flag
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __hip_atomic_store(a.bal_flags + tile * 2 + slot, a.bal_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            u = ue;
+        }
+        ts.mark(1);
+        return;
+    }
+    // owners: with two row tiles, bids b and b + 8 (one XCD) take the two row tiles of one
+    // W stripe (W read once into that XCD's L2); the remainder runs row tiles fastest
+    const int o = bid - n_lo;
+    int rt, ct;
+    if (m_tiles == 2 && o < (n_tiles / 16) * 16) {
+        rt = (o % 16) / 8;
+        ct = (o / 16) * 8 + o % 8;
+    } else {
+        rt = o % m_tiles;
+        ct = o / m_tiles;
+    }
+    const int tile = ct * m_tiles + rt, m0 = rt * kTile;
+    zero_acc(acc);
+    g3_run<EPI_SILU_MUL>(a, lds, m0, ct, 0, a.k / kK, 0, 2 * own, acc);
+    ts.mark(1);
+    const int w0 = worker_of(tile * P), nslots = worker_of(tile * P + P - 1) - w0 + 1;
+    __shared__ int ok_s[2];
+    if (t == 0) {
+        for (int sl = 0; sl < nslots; ++sl) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            int ok = 1;
+            while (__hip_atomic_load(a.bal_flags + tile * 2 + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                   a.bal_epoch) {
+                __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+                    if (a.err) atomicOr(a.err, 16);
+                    ok = 0;
+                    break;
+                }
+            }
+            ok_s[sl] = ok;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one L2 invalidate, then the barrier
+    }
+    __syncthreads();
+    for (int sl = 0; sl < nslots; ++sl) {
+        if (!ok_s[sl]) continue;
+        const float4* src = slot_ptr(tile, sl);
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const float4 p = src[(size_t)(((x * 2 + y) * 4 + i) * 2 + j) * kT];
+                        acc[x][y][i][j] += f4v{p.x, p.y, p.z, p.w};
+                    }
+    }
+    ts.mark(2);
+    g3_epilogue<EPI_SILU_MUL>(a, lds, acc, m0, ct, 0);
+}
+
+template <int EPI>
 int launch_g3(const Gemm2Args& a, int grid, hipStream_t s) {
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<EPI>),
@@ -457,6 +599,12 @@ int w8_prepare(const void* w16, int rows, int cols, void* w8, int* exp_out, hipS
     return LLMI_OK;
 }
 
+size_t gemm3_bal_slab_bytes(int m, int n) {
+    if (m <= 0 || n % 256 != 0) return 0;
+    const size_t tiles = (size_t)((m + kTile - 1) / kTile) * (n / 256);
+    return tiles * 2 * kTile * kTile * sizeof(float);
+}
+
 bool gemm3_supported(int n, int k, int epi, int ksplit) {
     const int ncols = (epi == EPI_SILU_MUL) ? n / 2 : n;
     const int tile = (epi == EPI_SILU_MUL) ? 128 : kTile;
@@ -492,6 +640,33 @@ int gemm3_launch(Gemm2Args a, hipStream_t s) {
     const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
     a.n_tiles = ncols / ((a.epi == EPI_SILU_MUL) ? 128 : kTile);
     const int grid = ((a.m + kTile - 1) / kTile) * a.n_tiles * a.ksplit;
+    if (a.epi == EPI_SILU_MUL && a.lo8 && a.bal_slab && a.bal_flags) {
+        // every CU busy: lo workers beside the tile owners, when the split is even enough
+        // (a tile touched by at most two workers) and the slots are large enough
+        // owner share `own` (pairs of lo tiles) so that owner (hi tiles + own pairs) and
+        // worker (their share of the rest) times meet; measured: an fp8 lo tile costs ~1.4x
+        // an fp16 one (2.2 vs 1.55 us in this kernel), i.e. a hi tile ~0.35 pairs
+        const int n_lo = a.bal_grid - grid, Pall = a.k / 256;
+        const double per = (double)grid / (n_lo > 0 ? n_lo : 1);  // tiles per worker
+        int own = (int)std::lround((Pall * per - 0.35 * (a.k / kK)) / (1.0 + per));
+        own = std::max(0, std::min(Pall - 1, own));
+        const int P = Pall - own, U = grid * P;
+        a.bal_own = own;
+        if (a.k % 256 == 0 && n_lo >= 1 && U / n_lo >= P &&
+            gemm3_bal_slab_bytes(a.m, a.n) > 0) {
+            static std::atomic<unsigned> epoch{0};
+            a.bal_epoch = ++epoch;
+            if (a.bal_epoch == 0) a.bal_epoch = ++epoch;  // 0 is the flags' initial value
+            static const bool attr = [] {
+                return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_silu_bal_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess;
+            }();
+            LLMI_REQUIRE(attr, "gemm3: cannot raise the dynamic LDS limit");
+            hipLaunchKernelGGL(gemm3_silu_bal_kernel, dim3(a.bal_grid), dim3(kT), kLds, s, a);
+            LLMI_HIP(hipGetLastError());
+            return LLMI_OK;
+        }
+    }
     switch (a.epi) {
         case EPI_STORE: return launch_g3<EPI_STORE>(a, grid, s);
         case EPI_ADD: return launch_g3<EPI_ADD>(a, grid, s);

@@ -103,7 +103,19 @@ struct Gemm2Args {
     int lo8 = 0;
     const void* w8 = nullptr;
     int w8_exp = 0;
+    // gemm3 EPI_SILU_MUL with lo8 only: spread the fp8 lo pass over the CUs the tiles leave
+    // idle (gemm3_silu_bal_kernel): bal_grid workgroups (the CU count), fp32 partial slots
+    // [tiles][2][256 x 256] and their flags [tiles][2] (zeroed once; epochs never repeat)
+    float* bal_slab = nullptr;
+    unsigned* bal_flags = nullptr;
+    int bal_grid = 0;
+    unsigned bal_epoch = 0;        // set by gemm3_launch
+    int bal_own = 0;               // set by gemm3_launch: lo tile pairs each owner keeps
+    int* err = nullptr;
+    unsigned long long* stamps = nullptr;  // debug timeline of the balanced kernel (WgStamp), null = off            // sticky error word (bit 16: a lo partial never arrived)
 };
+// bytes of the balanced gate_up's partial slots for m rows, n = 2 x intermediate (0: not used)
+size_t gemm3_bal_slab_bytes(int m, int n);
 // e4m3(W * 2^exp) of an fp16 [rows, cols] weight (exp chosen so that max |W| * 2^exp <= 448),
 // rows of 2 cols bytes with the first cols used (the fp16 row stride, gemm3.hip); synchronises s
 int w8_prepare(const void* w16, int rows, int cols, void* w8, int* exp_out, hipStream_t s);
@@ -231,7 +243,8 @@ struct DecodeState {
     int prompt_len;
     int vocab;
     int error;        // sticky error flags (1: token id out of range, 2: position overflow,
-                      // 4: host-sized attention grid != device position's split count)
+                      // 4: host-sized attention grid != device position's split count,
+                      // 16: a prefill gate_up lo partial never arrived, gemm3_silu_bal_kernel)
     int pad[3];
 };
 

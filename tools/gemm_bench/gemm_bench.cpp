@@ -105,6 +105,15 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&al, maxA * 2));
     CK(hipMalloc(&w, maxW * 2));
     CK(hipMalloc(&al8, maxA * 2));
+    float* bal_slab;
+    unsigned* bal_flags;
+    int* bal_err;
+    const size_t bal_bytes = gemm3_bal_slab_bytes(M, 22016);
+    CK(hipMalloc(&bal_slab, bal_bytes));
+    CK(hipMalloc(&bal_flags, 4096));
+    CK(hipMalloc(&bal_err, 4));
+    CK(hipMemset(bal_flags, 0, 4096));
+    CK(hipMemset(bal_err, 0, 4));
     CK(hipMalloc(&w8, maxW * 2));
     CK(hipMalloc(&y2, maxY * 4));
     CK(hipMalloc(&y3, maxY * 4));
@@ -126,14 +135,15 @@ int main(int argc, char** argv) {
         if (!only.empty() && only != s.name) continue;
         const int m = std::string(s.name) == "sq4096" ? 4096 : M;
         int w8e = 0;
-        if (only_planes == 0 || only_planes == 3) {
+        if (only_planes == 0 || only_planes >= 3) {
             if (w8_prepare(w, s.n, s.k, w8, &w8e, 0) != 0) return 1;
             hipLaunchKernelGGL(lo8_kernel, dim3(2048), dim3(256), 0, 0, al, (size_t)m, s.k, (unsigned char*)al8);
             CK(hipDeviceSynchronize());
         }
-        for (int pm = 1; pm <= 3; ++pm) {
+        for (int pm = 1; pm <= 4; ++pm) {  // 4: lo8 with the balanced gate_up (every CU busy)
             if (only_planes && pm != only_planes) continue;
-            const int planes = pm == 3 ? 2 : pm;
+            if (pm == 4 && s.epi != EPI_SILU_MUL) continue;
+            const int planes = pm >= 3 ? 2 : pm;
             Gemm2Args g;
             g.a[0] = ah; g.a[1] = al; g.planes = planes; g.lda = s.k; g.w = w; g.m = m; g.n = s.n; g.k = s.k;
             g.epi = s.epi; g.ksplit = s.ksplit; g.slab = slab; g.ldy = s.epi == EPI_SILU_MUL ? s.n / 2 : s.n;
@@ -145,7 +155,12 @@ int main(int argc, char** argv) {
             float us2 = -1.f;
             Gemm2Args g8 = g;  // the lo8 form of g (gemm3 only)
             g8.a[1] = al8; g8.lo8 = 1; g8.w8 = w8; g8.w8_exp = w8e;
-            if (pm == 3) {
+            if (pm == 4) {
+                int ncu = 0;
+                CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+                g8.bal_slab = bal_slab; g8.bal_flags = bal_flags; g8.bal_grid = ncu; g8.err = bal_err;
+            }
+            if (pm >= 3) {
                 float us3 = -1.f;
                 if (gemm3_supported(s.n, s.k, s.epi, s.ksplit) && s.k % 128 == 0 && s.k / 128 >= s.ksplit)
                     us3 = time_us([&] { gemm3_launch(g8, 0); }, iters);
@@ -197,9 +212,50 @@ int main(int argc, char** argv) {
                     }
                     err = mx / (ref > 0 ? ref : 1);
                 }
-                std::printf("{\"shape\": \"%s\", \"m\": %d, \"n\": %d, \"k\": %d, \"planes\": \"hi+lo8\", \"ksplit\": %d, "
-                            "\"w8_exp\": %d, \"exact_data\": %d, \"gemm3_us\": %.2f, \"rel_err\": %.3g}\n",
-                            s.name, m, s.n, s.k, s.ksplit, w8e, exact_data, us3, err);
+                int herr = 0;
+                CK(hipMemcpy(&herr, bal_err, 4, hipMemcpyDeviceToHost));
+                if (pm == 4) {  // one stamped launch: worker / owner timelines (us from the first start)
+                    unsigned long long* st;
+                    const int ng = g8.bal_grid;
+                    CK(hipMalloc(&st, (size_t)ng * 64));
+                    CK(hipMemset(st, 0, (size_t)ng * 64));
+                    Gemm2Args gs = g8;
+                    gs.stamps = st;
+                    gemm3_launch(gs, 0);
+                    CK(hipDeviceSynchronize());
+                    std::vector<unsigned long long> h((size_t)ng * 8);
+                    CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+                    const int n_lo = ng - 172;
+                    unsigned long long t0 = ~0ull;
+                    for (int b = 0; b < ng; ++b) t0 = std::min(t0, h[b * 8]);
+                    auto us = [&](unsigned long long v) { return (v - t0) / 100.0; };
+                    double wk_start_max = 0, wk_end_min = 1e9, wk_end_max = 0, ow_start_max = 0, ow_hi_min = 1e9,
+                           ow_hi_max = 0, ow_wait_max = 0, ow_end_max = 0;
+                    for (int b = 0; b < ng; ++b) {
+                        const unsigned long long* r = &h[b * 8];
+                        if (b < n_lo) {
+                            wk_start_max = std::max(wk_start_max, us(r[0]));
+                            wk_end_min = std::min(wk_end_min, us(r[1]));
+                            wk_end_max = std::max(wk_end_max, us(r[1]));
+                        } else {
+                            ow_start_max = std::max(ow_start_max, us(r[0]));
+                            ow_hi_min = std::min(ow_hi_min, us(r[1]));
+                            ow_hi_max = std::max(ow_hi_max, us(r[1]));
+                            ow_wait_max = std::max(ow_wait_max, us(r[2]));
+                            ow_end_max = std::max(ow_end_max, us(r[3]));
+                        }
+                    }
+                    std::printf("{\"timeline_us\": {\"workers\": %d, \"worker_start_max\": %.1f, \"worker_end\": [%.1f, %.1f], "
+                                "\"owner_start_max\": %.1f, \"owner_hi_done\": [%.1f, %.1f], \"owner_partials_in_max\": %.1f, "
+                                "\"owner_end_max\": %.1f}}\n",
+                                n_lo, wk_start_max, wk_end_min, wk_end_max, ow_start_max, ow_hi_min, ow_hi_max, ow_wait_max,
+                                ow_end_max);
+                    CK(hipFree(st));
+                }
+                std::printf("{\"shape\": \"%s\", \"m\": %d, \"n\": %d, \"k\": %d, \"planes\": \"%s\", \"ksplit\": %d, "
+                            "\"w8_exp\": %d, \"exact_data\": %d, \"gemm3_us\": %.2f, \"rel_err\": %.3g, \"err_word\": %d}\n",
+                            s.name, m, s.n, s.k, pm == 4 ? "hi+lo8 balanced" : "hi+lo8", s.ksplit, w8e, exact_data, us3, err,
+                            herr);
                 std::fflush(stdout);
                 continue;
             }

@@ -1,0 +1,23 @@
+#!/bin/bash
+# balanced gate_up (gemm3_silu_bal_kernel): exact-data check + timing vs the plain lo8
+# gate_up, the prefill tests, the prefill probe.   bash tools/gpu_bal.sh <tag>
+set -o pipefail
+TAG=${1:-bal}
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+OUT=gpurun_out; mkdir -p $OUT
+step() { echo "[$(date +%T)] $*"; }
+step "gate_up lo8 plain / balanced, exact data"
+timeout -k 10 60 ./tools/gemm_bench/gemm_bench_lo8 512 5 1 gate_up 3 1 > $OUT/bal_$TAG.jsonl || { echo "lo8 failed $?"; exit 1; }
+timeout -k 10 60 ./tools/gemm_bench/gemm_bench_lo8 512 5 1 gate_up 4 1 >> $OUT/bal_$TAG.jsonl || { echo "bal failed $?"; cat $OUT/bal_$TAG.jsonl; exit 1; }
+step "random data"
+timeout -k 10 60 ./tools/gemm_bench/gemm_bench_lo8 512 20 1 gate_up 3 0 >> $OUT/bal_$TAG.jsonl || { echo "lo8 failed $?"; exit 1; }
+timeout -k 10 60 ./tools/gemm_bench/gemm_bench_lo8 512 20 1 gate_up 4 0 >> $OUT/bal_$TAG.jsonl || { echo "bal failed $?"; cat $OUT/bal_$TAG.jsonl; exit 1; }
+cat $OUT/bal_$TAG.jsonl
+step "prefill tests"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_prefill.py -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_prefill_$TAG.log 2>&1 || { echo "prefill tests failed $?"; tail -40 $OUT/pytest_prefill_$TAG.log; exit 1; }
+grep -E "rel-L2|passed|failed" $OUT/pytest_prefill_$TAG.log
+step "prefill probe"
+timeout -k 10 300 python3 tools/prefill_probe.py 512 5 > $OUT/prefill_probe_$TAG.json 2>&1 || { echo "probe failed $?"; tail $OUT/prefill_probe_$TAG.json; exit 1; }
+cat $OUT/prefill_probe_$TAG.json
+step done
