@@ -415,9 +415,9 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
     g3_epilogue<EPI>(a, lds, acc, m0, ct, slice);
 }
 
-// gate_up in the fp8-lo mode with every CU busy (gemm3_launch with bal_slab): its 172
+// gate_up with two planes and every CU busy (gemm3_launch with bal_slab): its 172
 // 256 x 256 tiles alone leave 84 of 256 CUs idle for the whole launch. Workgroups
-// [0, n_lo) are lo workers: the fp8 lo pass of all tiles, in units of two 128-deep K tiles,
+// [0, n_lo) are lo workers: the lo pass of all tiles (fp8 or fp16), in units of two K tiles,
 // is split evenly over them (contiguous ranges that cross tile boundaries; a tile is
 // touched by at most two workers); each piece's fp32 partial goes to its tile's slot, then
 // a release fence and an epoch flag. Workgroups [n_lo, grid) own one tile each: its fp16
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kT) void gemm3_silu_bal_kernel(Gemm2Args a) {
     // a tile's first `own` pairs of 128-deep lo tiles stay with its owner (balance: an fp8
     // lo tile costs ~1.4 fp16 ones); the other P units go to the workers
     const int own = a.bal_own;
-    const int P = a.k / 256 - own;
+    const int P = a.k / (a.lo8 ? 256 : 128) - own;  // a unit = two lo tiles (128-deep fp8 or 64-deep fp16)
     const int U = n_tiles * P;
     auto worker_of = [&](int x) { return (int)(((long)(x + 1) * n_lo + U - 1) / U) - 1; };
     auto slot_ptr = [&](int tile, int slot) {
@@ -640,19 +640,21 @@ int gemm3_launch(Gemm2Args a, hipStream_t s) {
     const int ncols = (a.epi == EPI_SILU_MUL) ? a.n / 2 : a.n;
     a.n_tiles = ncols / ((a.epi == EPI_SILU_MUL) ? 128 : kTile);
     const int grid = ((a.m + kTile - 1) / kTile) * a.n_tiles * a.ksplit;
-    if (a.epi == EPI_SILU_MUL && a.lo8 && a.bal_slab && a.bal_flags) {
+    if (a.epi == EPI_SILU_MUL && a.planes == 2 && a.bal_slab && a.bal_flags) {
         // every CU busy: lo workers beside the tile owners, when the split is even enough
         // (a tile touched by at most two workers) and the slots are large enough
-        // owner share `own` (pairs of lo tiles) so that owner (hi tiles + own pairs) and
-        // worker (their share of the rest) times meet; measured: an fp8 lo tile costs ~1.4x
-        // an fp16 one (2.2 vs 1.55 us in this kernel), i.e. a hi tile ~0.35 pairs
-        const int n_lo = a.bal_grid - grid, Pall = a.k / 256;
+        // owner share `own` (units of two lo tiles) so that owner (hi tiles + own units) and
+        // worker (their share of the rest) times meet. A hi tile costs 0.5 unit against fp16
+        // lo tiles; against fp8 ones ~0.35 (measured: an fp8 lo tile costs ~1.4x an fp16
+        // one in this kernel, 2.2 vs 1.55 us)
+        const int n_lo = a.bal_grid - grid, Pall = a.k / (a.lo8 ? 256 : 128);
         const double per = (double)grid / (n_lo > 0 ? n_lo : 1);  // tiles per worker
-        int own = (int)std::lround((Pall * per - 0.35 * (a.k / kK)) / (1.0 + per));
+        const double hi_units = (a.lo8 ? 0.35 : 0.5) * (a.k / kK);
+        int own = (int)std::lround((Pall * per - hi_units) / (1.0 + per));
         own = std::max(0, std::min(Pall - 1, own));
         const int P = Pall - own, U = grid * P;
         a.bal_own = own;
-        if (a.k % 256 == 0 && n_lo >= 1 && U / n_lo >= P &&
+        if (a.k % (a.lo8 ? 256 : 128) == 0 && n_lo >= 1 && U / n_lo >= P &&
             gemm3_bal_slab_bytes(a.m, a.n) > 0) {
             static std::atomic<unsigned> epoch{0};
             a.bal_epoch = ++epoch;

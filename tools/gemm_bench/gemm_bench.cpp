@@ -140,9 +140,9 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL(lo8_kernel, dim3(2048), dim3(256), 0, 0, al, (size_t)m, s.k, (unsigned char*)al8);
             CK(hipDeviceSynchronize());
         }
-        for (int pm = 1; pm <= 4; ++pm) {  // 4: lo8 with the balanced gate_up (every CU busy)
+        for (int pm = 1; pm <= 5; ++pm) {  // 4 / 5: lo8 / fp16 lo with the balanced gate_up (every CU busy)
             if (only_planes && pm != only_planes) continue;
-            if (pm == 4 && s.epi != EPI_SILU_MUL) continue;
+            if (pm >= 4 && s.epi != EPI_SILU_MUL) continue;
             const int planes = pm >= 3 ? 2 : pm;
             Gemm2Args g;
             g.a[0] = ah; g.a[1] = al; g.planes = planes; g.lda = s.k; g.w = w; g.m = m; g.n = s.n; g.k = s.k;
@@ -155,7 +155,10 @@ int main(int argc, char** argv) {
             float us2 = -1.f;
             Gemm2Args g8 = g;  // the lo8 form of g (gemm3 only)
             g8.a[1] = al8; g8.lo8 = 1; g8.w8 = w8; g8.w8_exp = w8e;
-            if (pm == 4) {
+            if (pm == 5) {  // the fp16 two-plane gate_up, balanced: through the lo8 report path with lo8 off
+                g8 = g;
+            }
+            if (pm >= 4) {
                 int ncu = 0;
                 CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
                 g8.bal_slab = bal_slab; g8.bal_flags = bal_flags; g8.bal_grid = ncu; g8.err = bal_err;
@@ -194,9 +197,11 @@ int main(int argc, char** argv) {
                             const double v = ex ? std::ldexp(1.0 + mn / 8.0, ex - 7) : std::ldexp(mn / 8.0, -6);
                             return sg ? -v : v;
                         };
+                        const _Float16* l16 = reinterpret_cast<const _Float16*>(ll.data());
                         for (size_t i = 0; i < ny; ++i) {
                             const size_t r = i / g.ldy, cc = i % g.ldy;
-                            h3[i] = (float)((double)hh[i] + std::ldexp(e4m3(ll[r * 2 * g.ldy + cc]), -12));
+                            h3[i] = g8.lo8 ? (float)((double)hh[i] + std::ldexp(e4m3(ll[r * 2 * g.ldy + cc]), -12))
+                                           : (float)((double)hh[i] + (double)l16[i]);
                         }
                     } else {
                         Gemm2Args c3 = g8;
@@ -214,7 +219,7 @@ int main(int argc, char** argv) {
                 }
                 int herr = 0;
                 CK(hipMemcpy(&herr, bal_err, 4, hipMemcpyDeviceToHost));
-                if (pm == 4) {  // one stamped launch: worker / owner timelines (us from the first start)
+                if (pm >= 4) {  // one stamped launch: worker / owner timelines (us from the first start)
                     unsigned long long* st;
                     const int ng = g8.bal_grid;
                     CK(hipMalloc(&st, (size_t)ng * 64));
@@ -254,7 +259,7 @@ int main(int argc, char** argv) {
                 }
                 std::printf("{\"shape\": \"%s\", \"m\": %d, \"n\": %d, \"k\": %d, \"planes\": \"%s\", \"ksplit\": %d, "
                             "\"w8_exp\": %d, \"exact_data\": %d, \"gemm3_us\": %.2f, \"rel_err\": %.3g, \"err_word\": %d}\n",
-                            s.name, m, s.n, s.k, pm == 4 ? "hi+lo8 balanced" : "hi+lo8", s.ksplit, w8e, exact_data, us3, err,
+                            s.name, m, s.n, s.k, pm == 5 ? "hi+lo fp16 balanced" : pm == 4 ? "hi+lo8 balanced" : "hi+lo8", s.ksplit, w8e, exact_data, us3, err,
                             herr);
                 std::fflush(stdout);
                 continue;
