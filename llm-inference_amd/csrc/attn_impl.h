@@ -36,15 +36,19 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 
 // 8 cache elements of one row, as loaded (16 B for fp16, 32 B for fp32)
 template <typename KT> struct Raw { uint4 v[sizeof(KT) / 2]; };
+// K/V cache rows: non-temporal loads -- the cache (up to 1 GB at ctx 2048) is streamed once
+// per token and never fits the Infinity Cache. A/B on the 8-layer 7B loop (tools/ab_variants.sh,
+// profiles/r03m_attn_nt_ab.jsonl): 2-5 us per 8-layer token lower in 4 of 4 alternating pairs
+// (ctx 512 and 2048), though the attention kernel alone, layers cycled, reads 0.1-0.6 us slower
 __device__ __forceinline__ Raw<__half> ld_raw(const __half* p) {
     Raw<__half> r;
-    r.v[0] = *reinterpret_cast<const uint4*>(p);
+    r.v[0] = ld_nt16(p);
     return r;
 }
 __device__ __forceinline__ Raw<float> ld_raw(const float* p) {
     Raw<float> r;
-    r.v[0] = reinterpret_cast<const uint4*>(p)[0];
-    r.v[1] = reinterpret_cast<const uint4*>(p)[1];
+    r.v[0] = ld_nt16(p);
+    r.v[1] = ld_nt16(p + 4);
     return r;
 }
 __device__ __forceinline__ void unpack8(const Raw<__half>& r, float* v) {
