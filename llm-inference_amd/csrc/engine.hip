@@ -1322,6 +1322,7 @@ int llmi_engine_decode(llmi_engine* e, int n_steps, int use_graph) {
 
 int llmi_engine_prefill(llmi_engine* e, int n_tokens, int exact) {
     LLMI_REQUIRE(e, "null engine");
+    LLMI_REQUIRE(exact >= 0 && exact <= 2, "prefill: exact must be 0 (fp16 A), 1 (fp32-faithful) or 2 (fp8 lo planes)");
     LLMI_HIP(hipSetDevice(e->e.device));
     return e->e.prefill(n_tokens, exact == 2 ? 3 : exact ? 2 : 1);
 }

@@ -221,3 +221,13 @@ def test_prefill_rejects_rows_past_prompt():
         e.set_prompt(np.arange(1, 9, dtype=np.int32))
         with pytest.raises(_lib.LlmiError, match="inside the prompt"):
             e.prefill(9)
+
+
+def test_prefill_rejects_unknown_precision_mode():
+    """llmi_engine_prefill's exact is 0, 1 or 2 (include/llmi.h); the C ABI refuses others."""
+    cfg = preset("tiny")
+    with Engine(cfg) as e:
+        e.load_synthetic(1)
+        e.set_prompt(np.arange(1, 9, dtype=np.int32))
+        with pytest.raises(_lib.LlmiError, match="exact must be"):
+            _lib.call("llmi_engine_prefill", e._h, 8, 3)
