@@ -310,9 +310,10 @@ int llmi_engine_decode(llmi_engine* e, int n_steps, int use_graph);
  * n_tokens decode steps would have left it, so llmi_engine_decode continues.
  * exact = 1: fp32-faithful GEMMs (activations split into two fp16 halves);
  * exact = 2: the fp16 hi half exact, the remainder as e4m3 against e4m3 weight
- *   copies on the block-scaled fp8 MFMA (~1e-4 relative; the copies, 1 byte per
- *   GEMM weight, are made on the first such call; shapes without K % 128 == 0 fall
- *   back to exact = 1);
+ *   copies on the block-scaled fp8 MFMA (~1e-4 relative; the copies are made on the
+ *   first such call and kept at the fp16 row stride, i.e. as many bytes as the fp16
+ *   GEMM weights; an fp32 KV cache or shapes without K % 128 == 0 fall back to
+ *   exact = 1);
  * exact = 0: activations rounded to fp16 (faster, ~1e-3 relative at 32 layers).
  * Rows must lie inside the prompt; tp_world must be 1. fp32 weights run the
  * decode kernels row by row. */
