@@ -53,12 +53,6 @@ __device__ __forceinline__ float dot_packet(const uint4& w, const float4* xp, in
 }
 __device__ __forceinline__ float i8(uint32_t v, int j) { return (float)(int8_t)((v >> (8 * j)) & 0xff); }
 __device__ __forceinline__ float dot_packet(const uint4& w, const float4* xp, int nc, int8_t*) {
-#if LLMI_I8_DIAG == 1  // timing diagnostic only (wrong output): no dequantisation, x still read
-    const float4 x0 = xp[0];
-    return __uint_as_float((w.x ^ w.y ^ w.z ^ w.w) & 0x3f7fffffu) * x0.x;
-#elif LLMI_I8_DIAG == 2  // timing diagnostic only (wrong output): no dequantisation, no x reads
-    return __uint_as_float((w.x ^ w.y ^ w.z ^ w.w) & 0x3f7fffffu);
-#endif
     const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
     float s = 0.f;
 #pragma unroll
