@@ -16,13 +16,14 @@ import re
 import sys
 
 # Llama-2-7B prefill at M = 512: (kernel, workgroups) -> GEMM
-SHAPES = {("gemm3_kernel<2>", 172): "gate_up", ("gemm3_kernel<5>", 192): "qkv (2 K slices)",
+SHAPES = {("gemm3_kernel<2>", 172): "gate_up", ("gemm3_silu_bal_kernel", 256): "gate_up (fp8-lo, every CU)",
+          ("gemm3_kernel<5>", 192): "qkv (2 K slices)",
           ("gemm3_kernel<5>", 256): "down (8 K slices)", ("gemm2_kernel<128, 2, 5>", 256): "o_proj (2 K slices)",
           ("gemm2_kernel<128, 1, 5>", 256): "o_proj (2 K slices)"}
 
 
 def short(name):
-    m = re.search(r"(\w+_kernel(?:I\w+E|<[^>]*>))", name)
+    m = re.search(r"(\w+_kernel(?:I\w+E|<[^>]*>)?)", name)
     n = name if not m else m.group(1)
     return re.sub(r"\(.*", "", n.replace("void llmi::(anonymous namespace)::", ""))
 
