@@ -543,10 +543,17 @@ int launch_g3(const Gemm2Args& a, int grid, hipStream_t s) {
     return LLMI_OK;
 }
 
-__global__ void w8_amax_kernel(const __half* w, size_t n, unsigned* amax) {
+__global__ void w8_amax_kernel(const __half* w, size_t n, unsigned* amax) {  // n % 8 == 0, 16-B aligned
     float m = 0.f;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        m = fmaxf(m, fabsf(__half2float(w[i])));
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 8; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 u = reinterpret_cast<const uint4*>(w)[i];
+        const __half2* h = reinterpret_cast<const __half2*>(&u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float2 f = __half22float2(h[j]);
+            m = fmaxf(m, fmaxf(fabsf(f.x), fabsf(f.y)));
+        }
+    }
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));  // non-negative floats order as uints
 }
@@ -579,7 +586,7 @@ int w8_prepare(const void* w16, int rows, int cols, void* w8, int* exp_out, hipS
     unsigned* d = nullptr;
     LLMI_HIP(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(unsigned), s));
     LLMI_HIP(hipMemsetAsync(d, 0, sizeof(unsigned), s));
-    hipLaunchKernelGGL(w8_amax_kernel, dim3(1024), dim3(256), 0, s, static_cast<const __half*>(w16), count, d);
+    hipLaunchKernelGGL(w8_amax_kernel, dim3(2048), dim3(256), 0, s, static_cast<const __half*>(w16), count, d);
     unsigned bits = 0;
     LLMI_HIP(hipMemcpyAsync(&bits, d, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     LLMI_HIP(hipStreamSynchronize(s));
