@@ -231,3 +231,21 @@ def test_prefill_rejects_unknown_precision_mode():
         e.set_prompt(np.arange(1, 9, dtype=np.int32))
         with pytest.raises(_lib.LlmiError, match="exact must be"):
             _lib.call("llmi_engine_prefill", e._h, 8, 3)
+
+
+def test_prefill_fp8_lo_mode_13b_shape_matches_exact():
+    """exact=2 at Llama-2-13B width (other tile counts: 216 gate_up tiles, 40 lo workers,
+    owner share 12 of 20 unit pairs; K = 5120 and 13824) against exact=1 on the same engine:
+    the same greedy tokens after the prompt, logits within the mode's ~1e-4."""
+    cfg = preset("llama2-13b", layers=2, max_seq=320)
+    prompt = synth_prompt(5, 300, cfg.vocab)
+    out = {}
+    with Engine(cfg) as e:
+        e.load_synthetic(3)
+        for mode in (1, 2):
+            toks = e.generate(prompt, 8, prefill=True, exact=mode)
+            out[mode] = (toks.copy(), e.logits().copy())
+    np.testing.assert_array_equal(out[1][0], out[2][0])
+    r = rel(out[2][1], out[1][1])
+    print(f"13B-width fp8-lo vs exact prefill (+7 decode) logits rel-L2: {r:.3e}")
+    assert r < 5e-4
