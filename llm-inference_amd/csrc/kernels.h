@@ -232,7 +232,10 @@ __host__ __device__ __forceinline__ long long to_fixed(float v) {
 __host__ __device__ __forceinline__ float from_fixed(long long v) {
     return (float)v * 2.3283064365386963e-10f;  // (float) rounds once; * 2^-32 is exact
 }
-constexpr int kAttnChunk = 64;     // cached positions per workgroup (split-KV)
+#ifndef LLMI_ATTN_CH
+#define LLMI_ATTN_CH 64
+#endif
+constexpr int kAttnChunk = LLMI_ATTN_CH;  // cached positions per workgroup (split-KV)
 size_t attn_workspace_bytes(int heads, int head_dim, int max_seq);
 int attn_decode_launch(const AttnArgs& a, hipStream_t s);
 
