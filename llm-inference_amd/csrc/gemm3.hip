@@ -69,30 +69,13 @@ constexpr int kBuf = 4 * kHalf;      // A0 A1 B0 B1
 constexpr int kEpiRowB = 272;        // gate_up epilogue image: 128 halves + 16 B pad per row
 constexpr int kLds = 2 * kBuf > 2 * kTile * kEpiRowB ? 2 * kBuf : 2 * kTile * kEpiRowB;  // 136 KB
 
-#ifndef LLMI_G3_EXP
-#define LLMI_G3_EXP 0  // timing experiments only: 1 no DMA in the loop, 2 no LDS reads, 3 no DMA waits, 4 no stores
-#endif
-#ifndef LLMI_G3_LGKM_EARLY
-#define LLMI_G3_LGKM_EARLY 0
-#endif
 
 // LDS image swizzle (an involution): 16-B chunk c of 128-B row r is stored at chunk
 // c ^ ((r >> 1) & 7). A fragment ds_read_b128 (lane: row fr = lane & 15, chunk
 // 4 kk + (lane >> 4)) then puts the 16 lanes of each ds_read_b128 lane group on 16
 // distinct 16-B bank slots -- conflict-free (the st_16x32 XOR of gemm2 leaves it 2-way).
-#ifndef LLMI_G3_SWZ_OLD
 __device__ __forceinline__ int swz3(int b) { return b ^ (((b >> 8) & 7) << 4); }
-#else
-__device__ __forceinline__ int swz3(int b) { return b ^ (((b >> 9) & 1) << 5); }
-#endif
 
-__device__ __forceinline__ void glds(const void* g, unsigned lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
-}
 
 // the same with a uniform base in SGPRs and a 32-bit per-lane byte offset (saddr form):
 // no 64-bit per-lane pointers to keep live across the K loop
@@ -165,9 +148,6 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
     // issue the half-image `half` (0 A0, 1 A1, 2 B0, 3 B1) of virtual K tile v
     auto issue = [&](int v, int half) {
         if (v >= KT) return;
-#if LLMI_G3_EXP == 1
-        if (v >= 2) return;
-#endif
         const int plane = v >= nhi ? 1 : 0;
         const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (v & 1) * kBuf + half * kHalf + w * 1024);
         // fp8 rows keep the fp16 rows' byte stride (the first half of each row is used),
@@ -189,9 +169,6 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
 
     h8v af[4][2], b0[2][2], b1[2][2];
     auto read_a = [&](const char* img) {
-#if LLMI_G3_EXP == 2
-        if (KT > 0) return;
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -199,9 +176,6 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
                 af[i][kk] = *reinterpret_cast<const h8v*>(img + swz3((wr * 64 + i * 16 + fr) * 128 + kk * 64 + fq * 16));
     };
     auto read_b = [&](const char* img, h8v (&bf)[2][2]) {
-#if LLMI_G3_EXP == 2
-        if (KT > 0) return;
-#endif
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -236,12 +210,7 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
         __builtin_amdgcn_s_setprio(0);
     };
     auto sync_reads = [&](int n) {  // DMA counted, then the barrier; LDS reads retire behind it
-#if LLMI_G3_LGKM_EARLY
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-#if LLMI_G3_EXP != 3 && LLMI_G3_EXP != 1
         wait_vm(vm_count(n));
-#endif
         bar();
     };
 
@@ -409,9 +378,6 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
     f4v acc[2][2][4][2];
     zero_acc(acc);
     g3_run<EPI>(a, lds, m0, ct, kt0, KTs, lo8 ? kt0 / 2 : kt0, lo8 ? KTs / 2 : (a.planes == 2 ? KTs : 0), acc);
-#if LLMI_G3_EXP == 4
-    if (KTs > 0) return;  // timing experiment: no epilogue stores
-#endif
     g3_epilogue<EPI>(a, lds, acc, m0, ct, slice);
 }
 
