@@ -229,6 +229,8 @@ int llmi_synth_fill_host(void* out, int out_dtype, int kind, uint64_t seed, uint
 int llmi_device_alloc(void** ptr, size_t bytes);
 int llmi_device_free(void* ptr);
 int llmi_device_memset(void* ptr, int value, size_t bytes);
+/* stream-ordered form (hipMemsetAsync): the layer classes' scratch on their stream */
+int llmi_device_memset_async(void* ptr, int value, size_t bytes, llmi_stream_t stream);
 int llmi_memcpy(void* dst, const void* src, size_t bytes, int kind);
 int llmi_device_sync(void);
 
@@ -342,7 +344,20 @@ llmi_stream_t llmi_engine_stream(llmi_engine* e);
  * avg_us receives the mean duration; bytes the algorithmic bytes per launch. */
 int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us, uint64_t* bytes);
 /* which 8 / 9: the same residual exchange over the one-shot peer path (below), eager /
- * graph-replayed -- also a collective. */
+ * graph-replayed -- also a collective. which 10: the persistent ring layer (decode mode 1,
+ * below): o_proj + gate_up + down + the next layer's q/k/v in one launch. */
+
+/* Decode structure of a token (no reference counterpart: the reference launches ~326
+ * kernels per token). mode 0: 5 L + 2 launches (q/k/v, attention, o_proj, gate_up, down
+ * per layer). mode 1: the persistent ring layer -- per layer the attention launch plus
+ * ONE launch for o_proj, RMSNorm + gate_up + SiLU*up, down (K split by CU) and the next
+ * layer's RMSNorm + q/k/v, one workgroup per CU whose loader waves stream the weights
+ * through an LDS ring ahead of the in-launch hand-offs (2 L + 3 launches). Mode 1 needs
+ * fp16 weights, hidden 4096, head_dim 128, heads dividing the CU count and tp_world 1
+ * (else LLMI_EUNSUPPORTED); it keeps a transposed copy of every W_down (rebuilt after a
+ * weight load). The two modes differ only in the down projection's fp32 summation order.
+ * Graphs are re-captured. */
+int llmi_engine_set_decode_mode(llmi_engine* e, int mode);
 
 /* ---- One-shot peer exchange for tensor parallel decode (config 4; replaces the RCCL
  * all-reduces of the token graph: the sum of the row-parallel partials of

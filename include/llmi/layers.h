@@ -459,6 +459,8 @@ public:
     void freeBuf() {
         for (auto& t : bufs) allocator->Free(t->data, false);
         bufs.clear();
+        for (auto& t : hbufs) allocator->Free(t->data, false);
+        hbufs.clear();
     }
 
     // inputs: "attention_input" [num_tokens, H], "padding_offset", "history_length",
@@ -467,8 +469,9 @@ public:
     // [num_tokens, H], "all_k_cache" / "all_v_cache" [layers, bs, kv_heads, max_seq, head]
     void forward(TensorMap& inputs, TensorMap& outputs, LLaMAattentionWeights<T>& weights,
                  LLaMAAttentionDynParams& params, LLaMAAttentionStaticParams& static_params) {
-        LLM_CHECK_WITH_INFO(outputs["all_k_cache"]->dtype == FP32,
-                            "the context attention layer keeps an fp32 cache (the engine's prefill handles fp16)");
+        const DataType cdt = outputs["all_k_cache"]->dtype;
+        LLM_CHECK_WITH_INFO((cdt == FP32 || cdt == FP16) && outputs["all_v_cache"]->dtype == cdt,
+                            "the context attention layer's k/v caches must both be FP32 or both FP16");
         allocForForward(params);
         cublasWrapper cw{stream};
         cublasWrapper* c = cublas_wrapper ? cublas_wrapper : &cw;
@@ -477,8 +480,6 @@ public:
         TensorWrapper<int>* input_length = inputs["input_length"]->as<int>();
         TensorWrapper<int>* context_length = inputs["context_length"]->as<int>();
         TensorWrapper<int>* layer_id = inputs["layer_id"]->as<int>();
-        TensorWrapper<float>* all_k_cache = outputs["all_k_cache"]->as<float>();
-        TensorWrapper<float>* all_v_cache = outputs["all_v_cache"]->as<float>();
         llmi_detail::ActF32 in(inputs["attention_input"], allocator, stream, true, "LLaMAContextAttentionLayer");
         llmi_detail::ActF32 out(outputs["attention_output"], allocator, stream, false, "LLaMAContextAttentionLayer");
         // 1. qkv linear
@@ -486,11 +487,37 @@ public:
         // 2. RoPE (position history + s) and [num_tokens, ...] -> [bs, heads, max_q_len, head]
         launchAddFusedQKVBiasTransposeAndRoPE(q_buf_w_pad, k_buf_w_pad, v_buf_w_pad, qkv_buf_wo_pad, weights.qkv,
                                               padding_offset, history_length, input_length, static_params, stream);
-        // 3. append this prompt's k, v to the layer's cache after the history
-        launchConcatKVCache(k_buf_w_pad, v_buf_w_pad, layer_id, input_length, history_length, all_k_cache,
-                            all_v_cache, stream);
-        // 4. history + prompt, kv heads repeated to the query heads
-        launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, k_cache_buf, v_cache_buf, stream);
+        // positions past a sequence's context are never written by the repeat: zero them,
+        // so the masked columns of QK^T / PV multiply finite values
+        LLMI_CALL(llmi_device_memset_async(k_cache_buf->data, 0, k_cache_buf->size() * sizeof(float), stream));
+        LLMI_CALL(llmi_device_memset_async(v_cache_buf->data, 0, v_cache_buf->size() * sizeof(float), stream));
+        if (cdt == FP32) {
+            TensorWrapper<float>* all_k_cache = outputs["all_k_cache"]->as<float>();
+            TensorWrapper<float>* all_v_cache = outputs["all_v_cache"]->as<float>();
+            // 3. append this prompt's k, v to the layer's cache after the history
+            launchConcatKVCache(k_buf_w_pad, v_buf_w_pad, layer_id, input_length, history_length, all_k_cache,
+                                all_v_cache, stream);
+            // 4. history + prompt, kv heads repeated to the query heads
+            launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, k_cache_buf, v_cache_buf, stream);
+        } else {
+            // LLaMAContextAttentionLayer<half> (context_attention.cpp:177): the caches hold fp16.
+            // The new k/v rows are rounded to fp16 as they enter the cache (what the reference's
+            // half instantiation stores) and the repeated cache is widened back to fp32.
+            TensorWrapper<half_t>* all_k_cache = outputs["all_k_cache"]->as<half_t>();
+            TensorWrapper<half_t>* all_v_cache = outputs["all_v_cache"]->as<half_t>();
+            TensorWrapper<half_t>* kh = make_half(k_buf_w_pad->shape);
+            TensorWrapper<half_t>* vh = make_half(v_buf_w_pad->shape);
+            LLMI_CALL(llmi_convert(k_buf_w_pad->data, LLMI_F32, kh->data, LLMI_F16, kh->size(), stream));
+            LLMI_CALL(llmi_convert(v_buf_w_pad->data, LLMI_F32, vh->data, LLMI_F16, vh->size(), stream));
+            launchConcatKVCache(kh, vh, layer_id, input_length, history_length, all_k_cache, all_v_cache, stream);
+            TensorWrapper<half_t>* kr = make_half(k_cache_buf->shape);
+            TensorWrapper<half_t>* vr = make_half(v_cache_buf->shape);
+            LLMI_CALL(llmi_device_memset_async(kr->data, 0, kr->size() * sizeof(half_t), stream));
+            LLMI_CALL(llmi_device_memset_async(vr->data, 0, vr->size() * sizeof(half_t), stream));
+            launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, kr, vr, stream);
+            LLMI_CALL(llmi_convert(kr->data, LLMI_F16, k_cache_buf->data, LLMI_F32, kr->size(), stream));
+            LLMI_CALL(llmi_convert(vr->data, LLMI_F16, v_cache_buf->data, LLMI_F32, vr->size(), stream));
+        }
         launchLinearStridedBatchGemm(q_buf_w_pad, k_cache_buf, qk_buf, c, false, true);
         launchScaleMaskAndSoftmax(qk_buf, inputs["attention_mask"]->as<float>(), qk_buf, scale, stream);
         launchLinearStridedBatchGemm(qk_buf, v_cache_buf, qkv_buf_w_pad, c, false, false);
@@ -510,6 +537,15 @@ private:
         bufs.push_back(std::make_unique<TensorWrapper<float>>(GPU, FP32, shape, p));
         return bufs.back().get();
     }
+    TensorWrapper<half_t>* make_half(std::vector<int> shape) {  // fp16-cache staging
+        size_t n = 1;
+        for (int d : shape) n *= (size_t)d;
+        half_t* p = nullptr;
+        p = allocator->Malloc(p, sizeof(half_t) * n, false);
+        hbufs.push_back(std::make_unique<TensorWrapper<half_t>>(GPU, FP16, shape, p));
+        return hbufs.back().get();
+    }
+    std::vector<std::unique_ptr<TensorWrapper<half_t>>> hbufs;
     int head_num, kv_head_num, head_size, hidden_units, q_head_per_kv;
     float scale;
     LLaMAAttentionStaticParams attn_static_params;

@@ -242,6 +242,12 @@ int llmi_device_memset(void* ptr, int value, size_t bytes) {
     return LLMI_OK;
 }
 
+int llmi_device_memset_async(void* ptr, int value, size_t bytes, llmi_stream_t stream) {
+    LLMI_REQUIRE(ptr != nullptr || bytes == 0, "device_memset_async: null pointer");
+    if (bytes) LLMI_HIP(hipMemsetAsync(ptr, value, bytes, STREAM(stream)));
+    return LLMI_OK;
+}
+
 int llmi_memcpy(void* dst, const void* src, size_t bytes, int kind) {
     LLMI_REQUIRE(kind >= 0 && kind <= 2, "memcpy: kind must be 0 (H2D), 1 (D2H) or 2 (D2D)");
     const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost

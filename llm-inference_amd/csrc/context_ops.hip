@@ -303,32 +303,47 @@ __global__ __launch_bounds__(256) void bmm_kernel(const T* A, const T* B, T* C, 
 // layout). fp16 storage enters the MFMA exactly (P = 1). fp32 storage is split while it
 // is staged, v = hi + lo (hi = fp16(v), lo = fp16(v - hi)), on BOTH operands, and the
 // three products hi.hi + hi.lo + lo.hi are accumulated in fp32 (the lo.lo term is below
-// 2^-22 relative): fp32-faithful like gemm.hip's activation split.
+// 2^-22 relative): fp32-faithful like gemm.hip's activation split. fp16 has neither
+// fp32's range nor its small normals, so within each 32-deep K slab every row of A and
+// every column of B is first scaled by a power of two that puts its largest |value|
+// just below 2^14 (row maxima through LDS atomics); each output element of the slab's
+// MFMA product is scaled back by its row's and column's shifts while it is added in
+// fp32. Values of any fp32 magnitude thus keep hi + lo's precision relative to their
+// row's slab maximum (a row holding inf / NaN is left unscaled and yields inf / NaN, as
+// fp32 FMAs would).
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
 constexpr int kMT = 64, kMK = 32, kMLd = kMK + 8;  // tile, K slab, padded LDS row (halves)
+// exponent e with max|v| < 2^e (0 for an all-zero or non-finite slab: no scaling)
+__device__ __forceinline__ int slab_exp(unsigned max_bits) {
+    const float mx = __uint_as_float(max_bits);
+    if (max_bits == 0u || !(mx < INFINITY)) return 14;
+    int e;
+    (void)frexpf(mx, &e);
+    return e;
+}
 template <typename T, bool TA, bool TB>
 __global__ __launch_bounds__(256) void bmm_mfma_kernel(const T* A, const T* B, T* C, int m, int n, int k) {
     constexpr int P = std::is_same<T, float>::value ? 2 : 1;
     __shared__ __attribute__((aligned(16))) _Float16 As[P][kMT * kMLd];
     __shared__ __attribute__((aligned(16))) _Float16 Bs[P][kMT * kMLd];
+    __shared__ unsigned rmax[2][2][kMT];  // [slab parity][A rows, B columns]: max |v| bits in the slab
     const size_t z = blockIdx.z;
     A += z * m * (size_t)k;
     B += z * k * (size_t)n;
     C += z * m * (size_t)n;
     const int r0 = blockIdx.y * kMT, c0 = blockIdx.x * kMT;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+    for (int i = t; i < 4 * kMT; i += 256) (&rmax[0][0][0])[i] = 0u;
     // staging: 8 consecutive elements of the contiguous memory dimension per thread per
     // operand -- along k when k is contiguous (one 16-B LDS store), else along the rows
     // (8 scattered 2-B LDS stores); 16-B global loads where aligned and in bounds
-    auto stage = [&](const T* src, bool rows_contig, int rbase, int rlim, int ld_r, int ld_k, _Float16 (*dst)[kMT * kMLd],
-                     int k0) {
+    auto load = [&](const T* src, bool rows_contig, int rbase, int rlim, int ld_r, int ld_k, int k0, float (&v)[8]) {
         const int rr = rows_contig ? (t & 7) * 8 : t >> 2, kk = rows_contig ? t >> 3 : (t & 3) * 8;
         const int gr = rbase + rr, gk = k0 + kk;
         const T* p0 = src + (size_t)gr * ld_r + (size_t)gk * ld_k;
         const int lim = rows_contig ? rlim - gr : k - gk;              // elements left along the run
         const bool ok_other = rows_contig ? gk < k : gr < rlim;        // the fixed coordinate in range
-        float v[8];
         if (ok_other && lim >= 8 && (reinterpret_cast<uintptr_t>(p0) & 15) == 0) {
             if constexpr (sizeof(T) == 2) {
                 const h8_t h = *reinterpret_cast<const h8_t*>(p0);
@@ -343,11 +358,29 @@ __global__ __launch_bounds__(256) void bmm_mfma_kernel(const T* A, const T* B, T
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = (ok_other && e < lim) ? ldf(p0 + e) : 0.f;  // stride 1 along the run
         }
+    };
+    // |v| bits per tile row into LDS (non-negative floats order as integers; a NaN's bits
+    // exceed inf's, so it survives the max and leaves its row unscaled)
+    auto mark_max = [&](const float (&v)[8], bool rows_contig, unsigned* rm) {
+        if (rows_contig) {
+            const int rr = (t & 7) * 8;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) atomicMax(&rm[rr + e], __float_as_uint(fabsf(v[e])));
+        } else {
+            unsigned mx = 0u;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) mx = max(mx, __float_as_uint(fabsf(v[e])));
+            atomicMax(&rm[t >> 2], mx);
+        }
+    };
+    auto store = [&](const float (&v)[8], bool rows_contig, const unsigned* rm, _Float16 (*dst)[kMT * kMLd]) {
+        const int rr = rows_contig ? (t & 7) * 8 : t >> 2, kk = rows_contig ? t >> 3 : (t & 3) * 8;
         h8_t hi, lo;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            hi[e] = (_Float16)v[e];
-            lo[e] = (_Float16)(v[e] - (float)hi[e]);
+            const float s = P == 2 ? ldexpf(v[e], 14 - slab_exp(rm[rows_contig ? rr + e : rr])) : v[e];
+            hi[e] = (_Float16)s;
+            lo[e] = (_Float16)(s - (float)hi[e]);
         }
         if (!rows_contig) {
             *reinterpret_cast<h8_t*>(&dst[0][rr * kMLd + kk]) = hi;
@@ -366,10 +399,21 @@ __global__ __launch_bounds__(256) void bmm_mfma_kernel(const T* A, const T* B, T
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
     const int fr = lane & 15, fk = 8 * (lane >> 4);
-    for (int k0 = 0; k0 < k; k0 += kMK) {
+    __syncthreads();  // smax zeroed
+    for (int k0 = 0, it = 0; k0 < k; k0 += kMK, ++it) {
         // A element (r, kx): TA ? A[kx * m + r] : A[r * k + kx]; B element (c, kx): TB ? B[c * k + kx] : B[kx * n + c]
-        stage(A, TA, r0, m, TA ? 1 : k, TA ? m : 1, As, k0);
-        stage(B, !TB, c0, n, TB ? k : 1, TB ? 1 : n, Bs, k0);
+        float va[8], vb[8];
+        load(A, TA, r0, m, TA ? 1 : k, TA ? m : 1, k0, va);
+        load(B, !TB, c0, n, TB ? k : 1, TB ? 1 : n, k0, vb);
+        const int par = it & 1;
+        if constexpr (P == 2) {  // row scales of this slab: max |v| of every A row and B column
+            mark_max(va, TA, rmax[par][0]);
+            mark_max(vb, !TB, rmax[par][1]);
+            __syncthreads();
+            if (t < 2 * kMT) rmax[par ^ 1][t / kMT][t % kMT] = 0u;  // next slab's words: read after the next barrier
+        }
+        store(va, TA, rmax[par][0], As);
+        store(vb, !TB, rmax[par][1], Bs);
         __syncthreads();
         h8_t a[P][2], b[P][2];
 #pragma unroll
@@ -383,10 +427,18 @@ __global__ __launch_bounds__(256) void bmm_mfma_kernel(const T* A, const T* B, T
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
-                if constexpr (P == 2) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+                if constexpr (P == 2) {  // the slab's product, scaled back by its row and column shifts
+                    f4_t s = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][i], b[0][j], f4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    s = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][i], b[1][j], s, 0, 0, 0);
+                    s = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1][i], b[0][j], s, 0, 0, 0);
+                    const int shb = 14 - slab_exp(rmax[par][1][wc * 32 + 16 * j + fr]);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int sha = 14 - slab_exp(rmax[par][0][wr * 32 + 16 * i + 4 * (lane >> 4) + q]);
+                        acc[i][j][q] += ldexpf(s[q], -(sha + shb));
+                    }
+                } else {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
                 }
             }
         __syncthreads();

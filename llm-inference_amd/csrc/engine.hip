@@ -168,6 +168,19 @@ struct Engine {
     float* pf_bal = nullptr;
     unsigned* pf_bal_flags = nullptr;
     int n_cu = 0;
+    // decode mode 1: the persistent ring layer (ring.hip) -- per token step_start, q/k/v(0),
+    // L x [attention, ring], lm_head. rl_acc holds the int64 residual accumulators in
+    // five slots [A0][A1][B0][A2][B1] (A: layer inputs x_l, slot l % 3; B: mid-layer sums,
+    // slot l % 2), A1 + B0 adjacent so step_start zeroes both; rl_cnt the per-layer fan-in
+    // counters; wdt the transposed W_down copies the ring's K split reads.
+    int decode_mode = 0;
+    long long* rl_acc = nullptr;
+    unsigned* rl_cnt = nullptr;
+    char* wdt_blob = nullptr;
+    bool wdt_valid = false;
+    long long* acc_a(int l) const { static const int s[3] = {0, 1, 3}; return rl_acc + (size_t)s[l % 3] * c.hidden; }
+    long long* acc_b(int l) const { return rl_acc + (size_t)(l % 2 ? 4 : 2) * c.hidden; }
+    void* wdt_of(int l) const { return wdt_blob + (size_t)l * il * c.hidden * 2; }
     int host_next_pos = 0, prompt_len = 0;
     unsigned long long* dbg_stamps = nullptr;  // llmi_engine_debug_stamps: per-workgroup timeline
     // llmi_engine_debug_timeline: every stamped launch of a recorded step gets its own
@@ -203,6 +216,9 @@ struct Engine {
         if (w8blob) (void)hipFree(w8blob);
         if (pf_bal) (void)hipFree(pf_bal);
         if (pf_bal_flags) (void)hipFree(pf_bal_flags);
+        if (rl_acc) (void)hipFree(rl_acc);
+        if (rl_cnt) (void)hipFree(rl_cnt);
+        if (wdt_blob) (void)hipFree(wdt_blob);
         if (stream && own_stream) (void)hipStreamDestroy(stream);
     }
 
@@ -367,7 +383,21 @@ struct Engine {
     }
 
     // ----------------------------------------------------------- weights
+    // Every copy derived from the weights (the split-3 prefill's e4m3 copies) is dropped
+    // before any weight is written; it is rebuilt from the new weights on next use.
+    int weights_changed() {
+        wdt_valid = false;  // the ring's W_down^T copies are rebuilt before the next ring decode
+        if (w8blob) {
+            LLMI_HIP(hipStreamSynchronize(stream));  // a prefill may still read them
+            LLMI_HIP(hipFree(w8blob));
+            w8blob = nullptr;
+            w8l.clear();
+        }
+        return LLMI_OK;
+    }
+
     int load_synthetic(uint64_t sd) {
+        LLMI_TRY(weights_changed());
         seed = sd;
         const int H = c.hidden, r = c.tp_rank;
         const int lin = (wdt == LLMI_I8) ? LLMI_SYN_INT8 : LLMI_SYN_LINEAR;
@@ -438,6 +468,7 @@ struct Engine {
     // name: the reference's file stem without ".bin" (e.g. "model.layers.3.self_attn.qkv.weight")
     int load_tensor(const char* name, const float* src, size_t count) {
         LLMI_REQUIRE(name && src, "load_tensor: null argument");
+        LLMI_TRY(weights_changed());
         const std::string nm(name);
         const size_t H = c.hidden, D = c.head_dim, QR = (size_t)c.heads * D, KR = (size_t)c.kv_heads * D;
         const size_t I = c.inter, r = c.tp_rank;
@@ -511,12 +542,6 @@ struct Engine {
     // Llama<T>::loadWeights(weight_path): weight_path + "<name>.bin" for every tensor.
     int load_bin(const char* weight_path) {
         LLMI_REQUIRE(weight_path, "load_bin: null path");
-        if (w8blob) {  // the fp8 copies follow the weights: rebuilt at the next split-3 prefill
-            LLMI_HIP(hipStreamSynchronize(stream));
-            LLMI_HIP(hipFree(w8blob));
-            w8blob = nullptr;
-            w8l.clear();
-        }
         std::vector<std::string> names = {"model.norm.weight", "lm_head.weight", "model.embed_tokens.weight"};
         for (int l = 0; l < c.layers; ++l)
             for (const char* leaf : {"input_layernorm.weight", "post_attention_layernorm.weight",
@@ -745,8 +770,92 @@ struct Engine {
         return LLMI_OK;
     }
 
+    // ------------------------------------------------ persistent ring layer (mode 1)
+    bool ring_ok() const {
+        return wdt == LLMI_F16 && edt == LLMI_F16 && c.tp_world == 1 && !grouped &&
+               ring_supported(c.hidden, hl, c.head_dim, il, ql + 2 * kvrows, n_cu);
+    }
+    int set_decode_mode(int mode) {
+        LLMI_REQUIRE(mode == 0 || mode == 1, "set_decode_mode: mode must be 0 (launches) or 1 (ring layer)");
+        LLMI_HIP(hipStreamSynchronize(stream));
+        if (mode == 1) {
+            if (n_cu == 0) LLMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+            if (!ring_ok()) {
+                set_last_error("[llmi][ERROR] set_decode_mode: the ring layer needs fp16 weights, hidden 4096, "
+                               "head_dim 128, heads dividing the CU count, tp_world 1");
+                return LLMI_EUNSUPPORTED;
+            }
+            int per_cu = 0;
+            LLMI_TRY(ring_residency(&per_cu));
+            LLMI_REQUIRE(per_cu >= 1, "set_decode_mode: the ring layer's workgroup does not fit a CU");
+            if (!rl_acc) {
+                LLMI_HIP(hipMalloc(&rl_acc, (size_t)5 * c.hidden * 8));
+                LLMI_HIP(hipMalloc(&rl_cnt, (size_t)c.layers * kRingCntWords * 4));
+                LLMI_HIP(hipMalloc(&wdt_blob, (size_t)c.layers * il * c.hidden * 2));
+            }
+            LLMI_HIP(hipMemset(rl_acc, 0, (size_t)5 * c.hidden * 8));
+            LLMI_HIP(hipMemset(rl_cnt, 0, (size_t)c.layers * kRingCntWords * 4));
+        }
+        graphs.clear();  // the captured steps change
+        decode_mode = mode;
+        return LLMI_OK;
+    }
+    int prepare_ring() {  // W_down^T of every layer, from the current weights
+        if (wdt_valid) return LLMI_OK;
+        for (int l = 0; l < c.layers; ++l) LLMI_TRY(transpose_f16_launch(layers[l].down, wdt_of(l), c.hidden, il, stream));
+        LLMI_HIP(hipStreamSynchronize(stream));
+        wdt_valid = true;
+        return LLMI_OK;
+    }
+    // ring launch of layer l; wrap: the timing loop's cyclic form (every launch has a
+    // q/k/v phase and prepares layer (l + 1) % L's state)
+    RingArgs ring_args(int l, bool wrap = false) const {
+        const int L = c.layers;
+        const bool next = l + 1 < L || wrap;
+        const Layer& Lw = layers[l];
+        RingArgs r;
+        r.w_o = Lw.o; r.w_gu = Lw.gu; r.w_dt = wdt_of(l); r.g_ffn = Lw.ffn_norm;
+        if (next) {
+            r.w_qkv = layers[(l + 1) % L].qkv;
+            r.g_attn = layers[(l + 1) % L].attn_norm;
+            r.qkv_out = qkv_buf;
+        }
+        r.attn_ws = attn_ws;
+        r.acc_x = acc_a(l); r.acc_mid = acc_b(l); r.acc_out = acc_a(l + 1);
+        r.zero0 = next ? acc_b(l + 1) : nullptr;
+        r.zero1 = (l + 2 <= L || wrap) ? acc_a(l + 2) : nullptr;
+        r.cnt = rl_cnt + (size_t)l * kRingCntWords;
+        r.cnt_zero = rl_cnt + (size_t)((l + 1) % L) * kRingCntWords;
+        r.hidden = c.hidden; r.heads = hl; r.inter = il; r.n_qkv = ql + 2 * kvrows; r.max_seq = c.max_seq;
+        r.nact = rec_nact; r.eps = c.rms_eps; r.err = &st->error;
+        r.stamps = stamp_ptr();
+        return r;
+    }
+    int record_step_ring() {
+        dbg_slot = 0;
+        // step_start: x_0 into slot A0, zero A1 + B0 (adjacent) for layer 0's sums
+        LLMI_TRY(step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, acc_a(0), c.max_seq,
+                                   reinterpret_cast<unsigned*>(acc_a(1)), 4 * c.hidden, stream));
+        GemvArgs q = qkv_args(0);
+        q.x_fixed = acc_a(0);
+        LLMI_TRY(gemv_launch(q, stream));
+        for (int l = 0; l < c.layers; ++l) {
+            AttnArgs at = attn_args(l);
+            at.xacc = nullptr;  // the ring seeds the o_proj sum itself
+            LLMI_TRY(attn_decode_launch(at, stream));
+            LLMI_TRY(ring_layer_launch(ring_args(l), n_cu, stream));
+        }
+        GemvArgs h = lm_args();
+        h.x_fixed = acc_a(c.layers);
+        LLMI_TRY(gemv_launch(h, stream));
+        if (sample_k == 0) return LLMI_OK;
+        LLMI_TRY(topk_launch(logits, LLMI_F32, 1, c.vocab, sample_k, samp_ids, samp_vals, stream));
+        return sample_pick_launch(st, samp_ids, samp_vals, sample_k, sample_seed, partials, lm_grid, stream);
+    }
+
     int record_step() {
         LLMI_REQUIRE(!grouped, "engine: a group rank is stepped by its group");
+        if (decode_mode == 1) return record_step_ring();
         dbg_slot = 0;
         LLMI_TRY(rec_start());
         for (int l = 0; l < c.layers; ++l) {
@@ -789,6 +898,7 @@ struct Engine {
         LLMI_REQUIRE(c.tp_world == 1 || comm || xchg_mode == 1,
                      "decode: tp_world > 1 needs an RCCL id at create or the one-shot exchange (xchg_open + set_exchange)");
         LLMI_REQUIRE(n >= 0 && host_next_pos + n <= c.max_seq, "decode: would run past max_seq");
+        if (decode_mode == 1 && n > 0) LLMI_TRY(prepare_ring());
         if (use_graph && n > 0)  // every graph this run replays, captured before the first launch
             for (int k = nact_of(host_next_pos); k <= nact_of(host_next_pos + n - 1); ++k) LLMI_TRY(build_graph(k));
         for (int i = 0; i < n; ++i) {
@@ -835,9 +945,14 @@ struct Engine {
         pf_qkv = (float*)(pf + oq);
         pf_o = (float*)(pf + oo);
         pf_act = (float*)(pf + oa);
-        // the two-plane gate_up on every CU (gemm3_silu_bal_kernel): lo partial slots + flags
-        const size_t sb = gemm3_bal_slab_bytes(pf_rows, 2 * il);
         LLMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+        return LLMI_OK;
+    }
+    // split mode 3's gate_up on every CU (gemm3_silu_bal_kernel): lo partial slots + flags,
+    // allocated on the first split-3 prefill (~88 MB at 7B; the other modes never read them)
+    int alloc_bal() {
+        if (pf_bal) return LLMI_OK;
+        const size_t sb = gemm3_bal_slab_bytes(pf_rows, 2 * il);
         if (sb > 0) {
             const size_t nflags = sb / ((size_t)256 * 256 * 4);  // two slots per tile, one flag each
             LLMI_HIP(hipMalloc(&pf_bal, sb));
@@ -990,7 +1105,10 @@ struct Engine {
                                gemm2_supported(c.hidden, ql, EPI_ADD) && gemm2_supported(2 * il, c.hidden, EPI_SILU_MUL) &&
                                gemm2_supported(c.hidden, il, EPI_ADD) && c.head_dim % 64 == 0;
         if (split == 3 && !(use_gemm2 && lo8_supported())) split = 2;  // shapes without the fp8 lo pass: exact planes
-        if (split == 3) LLMI_TRY(alloc_w8());
+        if (split == 3) {
+            LLMI_TRY(alloc_w8());
+            LLMI_TRY(alloc_bal());
+        }
         const int H = c.hidden, p_begin = host_next_pos;
         const size_t eb = dtype_size(c.kv_dtype);
         for (int p0 = p_begin; p0 < p_begin + n; p0 += pf_rows) {
@@ -1060,7 +1178,8 @@ struct Engine {
         LLMI_HIP(hipMemcpy(&h, st, sizeof(h), hipMemcpyDeviceToHost));
         LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error) +
                                        " (1: token id out of range, 2: position overflow, 4: attention split count != device position, "
-                                       "16: a prefill gate_up lo partial never arrived)");
+                                       "8: a tensor-parallel peer never arrived (one-shot exchange timeout), "
+                                       "16: a prefill gate_up lo partial never arrived, 32: a ring-layer hand-off timed out)");
         const int m = n < valid ? n : valid;
         if (m > 0) LLMI_HIP(hipMemcpy(out, tokens, (size_t)m * 4, hipMemcpyDeviceToHost));
         if (n_valid) *n_valid = valid;
@@ -1423,6 +1542,12 @@ int llmi_engine_xchg_open(llmi_engine* e, const void* handles) {
     return LLMI_OK;
 }
 
+int llmi_engine_set_decode_mode(llmi_engine* e, int mode) {
+    LLMI_REQUIRE(e, "set_decode_mode: null engine");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.set_decode_mode(mode);
+}
+
 int llmi_engine_set_exchange(llmi_engine* e, int mode) {
     LLMI_REQUIRE(e, "set_exchange: null engine");
     LLMI_HIP(hipSetDevice(e->e.device));
@@ -1502,12 +1627,15 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             case 8:
             case 9:  // the same exchange over the one-shot peer path
                 return llmi::xchg_launch(g.xchg_args(g.xacc, (int)H, 0, 3), g.stream);
+            case 10:  // the persistent ring layer (o_proj, gate_up, down, next q/k/v)
+                return llmi::ring_layer_launch(g.ring_args(l, true), g.n_cu, g.stream);
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..9");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..10");
     };
     LLMI_REQUIRE(which < 6 || which > 7 || g.comm != nullptr,
                  "time_kernel: the all-reduce needs an RCCL communicator (tp_id)");
-    LLMI_REQUIRE(which < 8 || g.peers_ready, "time_kernel: the one-shot exchange needs xchg_open");
+    LLMI_REQUIRE(which < 8 || which > 9 || g.peers_ready, "time_kernel: the one-shot exchange needs xchg_open");
+    LLMI_REQUIRE(which != 10 || (g.decode_mode == 1 && g.wdt_valid), "time_kernel: the ring layer needs decode mode 1");
     const uint64_t ws = g.wsz, sc = (g.wdt == LLMI_I8) ? 2 : 0;
     switch (which) {
         case 0: b = (uint64_t)(g.ql + 2 * g.kvrows) * H * ws + (g.ql + 2 * g.kvrows) * sc; break;
@@ -1526,6 +1654,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
         case 7:
         case 8:
         case 9: b = (uint64_t)H * 8; break;
+        case 10: b = ((uint64_t)H * g.ql + 3ull * g.il * H + (uint64_t)(g.ql + 2 * g.kvrows) * H) * ws; break;
     }
     // timing launches modify the residual stream (o/down epilogues add into x),
     // so save and restore the small activation state around them
@@ -1551,6 +1680,11 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             for (int v = 0; v < 2; ++v)
                 LLMI_HIP(hipMemcpy2D(save_kv.data() + ((size_t)l * 2 + v) * g.kvl * kv_row, kv_row, kv_rows(l, v),
                                      kv_pitch, kv_row, g.kvl, hipMemcpyDeviceToHost));
+    }
+    std::vector<char> save_rl;
+    if (which == 10) {
+        save_rl.resize((size_t)5 * H * 8);
+        LLMI_HIP(hipMemcpyAsync(save_rl.data(), g.rl_acc, save_rl.size(), hipMemcpyDeviceToHost, g.stream));
     }
     LLMI_TRY(launch());  // warm
     hipGraph_t cg = nullptr;
@@ -1586,6 +1720,10 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
             for (int v = 0; v < 2; ++v)
                 LLMI_HIP(hipMemcpy2D(kv_rows(l, v), kv_pitch, save_kv.data() + ((size_t)l * 2 + v) * g.kvl * kv_row,
                                      kv_row, kv_row, g.kvl, hipMemcpyHostToDevice));
+    if (which == 10) {  // accumulators back, every layer's counters zero again
+        LLMI_HIP(hipMemcpy(g.rl_acc, save_rl.data(), save_rl.size(), hipMemcpyHostToDevice));
+        LLMI_HIP(hipMemset(g.rl_cnt, 0, (size_t)g.c.layers * llmi::kRingCntWords * 4));
+    }
     *avg_us = ms * 1000.f / iters;
     if (bytes) *bytes = b;
     return LLMI_OK;

@@ -26,8 +26,8 @@
 // (P = 2 issues 2x that on the matrix cores).
 #include <algorithm>
 #include <cstdlib>
+#include <map>
 #include <mutex>
-#include <unordered_map>
 #include <utility>
 
 #include "kernels.h"
@@ -445,12 +445,20 @@ __global__ __launch_bounds__(kThreads) void slab_sum_kernel(const float4* slab, 
         y[i] = a;
     }
 }
+// keyed by (device, stream): the null stream is the same handle on every device
 std::mutex g_ws_mu;
-std::unordered_map<hipStream_t, std::pair<void*, size_t>> g_ws;
+std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> g_ws;
 int linear_workspace(hipStream_t s, size_t bytes, char** out) {
+    int dev = 0;
+    LLMI_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(g_ws_mu);
-    auto& e = g_ws[s];
+    auto& e = g_ws[{dev, s}];
     if (bytes > e.second) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        LLMI_HIP(hipStreamIsCapturing(s, &cap));
+        LLMI_REQUIRE(cap == hipStreamCaptureStatusNone,
+                     "linear_mfma: the workspace must grow, which cannot happen while the stream is capturing "
+                     "(run the same shapes once before capture)");
         if (e.first) {  // earlier launches on this stream may still read it
             LLMI_HIP(hipStreamSynchronize(s));
             LLMI_HIP(hipFree(e.first));

@@ -221,6 +221,42 @@ struct OprojArgs {
     int nact = 0;  // > 0: active split count known on the host (no position read); see AttnArgs
 };
 int attn_oproj_launch(const OprojArgs& a, hipStream_t s);
+
+// Persistent ring layer (ring.hip): after layer l's attention, ONE launch runs
+//   o_proj (merge fused, by head) -> RMSNorm + gate_up + SiLU*up -> down (K split by CU)
+//   -> [RMSNorm + next layer's q/k/v]
+// on one workgroup per CU whose loader waves stream every weight the CU needs into an
+// LDS ring, running ahead across the two in-launch hand-offs (the o_proj and down sums,
+// int64 fixed-point atomics + a sharded arrival counter). fp16 weights, hidden 4096.
+constexpr int kRingShards = 8, kRingShardWords = 32;           // one 128-B line per shard
+constexpr int kRingCntWords = 2 * kRingShards * kRingShardWords;  // a layer's two fan-in counters
+struct RingArgs {
+    const void* w_o = nullptr;      // [hidden][heads * 128] fp16
+    const void* w_gu = nullptr;     // [2 inter][hidden] fp16 (gate rows, then up rows)
+    const void* w_dt = nullptr;     // [inter][hidden] fp16: W_down transposed
+    const void* w_qkv = nullptr;    // next layer's [n_qkv][hidden] fp16; null: no q/k/v phase
+    const void* g_ffn = nullptr;    // this layer's post-attention RMSNorm gamma (fp16)
+    const void* g_attn = nullptr;   // next layer's input RMSNorm gamma (fp16)
+    const void* attn_ws = nullptr;  // this layer's split-KV attention partials (attn_impl.h Ws)
+    long long* acc_x = nullptr;     // x_l (fixed point, read)
+    long long* acc_mid = nullptr;   // x_l + o_proj (atomics; zero at launch)
+    long long* acc_out = nullptr;   // x_{l+1} = mid + down (atomics; zero at launch)
+    long long* zero0 = nullptr;     // accumulators of the next launches, zeroed here (may be null)
+    long long* zero1 = nullptr;
+    unsigned* cnt = nullptr;        // this layer's counters [2][kRingShards][kRingShardWords] (zero at launch)
+    unsigned* cnt_zero = nullptr;   // the next ring launch's counters, zeroed here
+    float* qkv_out = nullptr;       // next layer's q/k/v rows (fp32)
+    int hidden = 0, heads = 0, inter = 0, n_qkv = 0, max_seq = 0, nact = 0;
+    float eps = 1e-5f;
+    int* err = nullptr;             // DecodeState::error: bit 32 = a hand-off wait timed out
+    unsigned long long* stamps = nullptr;  // per-CU timeline [8] (null = off)
+};
+bool ring_supported(int hidden, int heads, int head_dim, int inter, int n_qkv, int n_cu);
+int ring_layer_launch(const RingArgs& a, int grid, hipStream_t s);
+int ring_residency(int* per_cu);  // workgroups of the ring kernel one CU admits (must be >= 1)
+// W_down [rows][cols] fp16 -> its transpose [cols][rows] (the ring's K split by CU)
+int transpose_f16_launch(const void* src, void* dst, int rows, int cols, hipStream_t s);
+
 // fixed-point residual accumulator: value = int64 * 2^-32
 __host__ __device__ __forceinline__ long long to_fixed(float v) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -247,7 +283,9 @@ struct DecodeState {
     int vocab;
     int error;        // sticky error flags (1: token id out of range, 2: position overflow,
                       // 4: host-sized attention grid != device position's split count,
-                      // 16: a prefill gate_up lo partial never arrived, gemm3_silu_bal_kernel)
+                      // 8: a tensor-parallel peer never arrived (one-shot exchange timeout, xchg.hip),
+                      // 16: a prefill gate_up lo partial never arrived, gemm3_silu_bal_kernel,
+                      // 32: a ring-layer hand-off or ring-slot wait timed out, ring.hip)
     int pad[3];
 };
 

@@ -64,6 +64,7 @@ _SIGS = {
     "llmi_synth_prompt": (_I, [_U64, _I, _I, _P]),
     "llmi_device_alloc": (_I, [C.POINTER(_P), _SZ]),
     "llmi_device_memset": (_I, [_P, _I, _SZ]),
+    "llmi_device_memset_async": (_I, [_P, _I, _SZ, _P]),
     "llmi_device_free": (_I, [_P]),
     "llmi_memcpy": (_I, [_P, _P, _SZ, _I]),
     "llmi_device_sync": (_I, []),
@@ -96,6 +97,7 @@ _SIGS = {
     "llmi_engine_xchg_handle": (_I, [_P, _P]),
     "llmi_engine_xchg_open": (_I, [_P, _P]),
     "llmi_engine_set_exchange": (_I, [_P, _I]),
+    "llmi_engine_set_decode_mode": (_I, [_P, _I]),
     "llmi_group_set_exchange": (_I, [_P, _I]),
     "llmi_group_create": (_I, [C.POINTER(Config), _I, _I, C.POINTER(_P)]),
     "llmi_group_destroy": (_I, [_P]),

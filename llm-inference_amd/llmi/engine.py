@@ -135,7 +135,7 @@ class Engine:
     # allreduce / allreduce_graph: one residual all-reduce of the TP exchange (needs a tp_id),
     # launched eagerly / replayed from a captured graph of `iters` calls
     KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5, "allreduce": 6,
-               "allreduce_graph": 7, "xchg": 8, "xchg_graph": 9}
+               "allreduce_graph": 7, "xchg": 8, "xchg_graph": 9, "ring": 10}
 
     # one-shot peer exchange (tensor parallel without RCCL in the token graph)
     def xchg_handle(self) -> bytes:
@@ -153,6 +153,11 @@ class Engine:
     def set_exchange(self, mode: int):
         """0: RCCL all-reduces (needs a tp_id at create); 1: the one-shot peer exchange."""
         call("llmi_engine_set_exchange", self._h, int(mode))
+
+    def set_decode_mode(self, mode: int):
+        """0: five launches per layer; 1: the persistent ring layer (ring.hip: attention +
+        one launch per layer). Raises LlmiError where mode 1 is unsupported."""
+        call("llmi_engine_set_decode_mode", self._h, int(mode))
 
     def time_kernel(self, which: str, iters: int = 50):
         us, b = C.c_float(), C.c_uint64()

@@ -4,7 +4,9 @@
 // after them (rope at history + t, KV concat at slot history + t, causal mask over
 // history + chunk). Inputs from <dir>/*.bin, outputs to <dir>/out_*.bin for the pytest
 // driver (tests/test_gpu_ctx_history.py):
-//   test_ctx_history <dir> <heads> <kv_heads> <head> <inter> <layers> <vocab> <max_seq> <seed> <bs>
+//   test_ctx_history <dir> <heads> <kv_heads> <head> <inter> <layers> <vocab> <max_seq> <seed> <bs> [f16]
+// With "f16" the caches are TensorWrapper<half> (LLaMAContextAttentionLayer<half>,
+// context_attention.cpp:177): uploaded rounded to fp16, written back widened to fp32.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -49,6 +51,7 @@ int main(int argc, char** argv) {
         const int L = std::atoi(argv[6]), V = std::atoi(argv[7]), S = std::atoi(argv[8]);
         const uint64_t seed = std::strtoull(argv[9], nullptr, 10);
         const int bs = std::atoi(argv[10]);
+        const bool f16 = argc > 11 && std::string(argv[11]) == "f16";
         const int H = heads * hd;
         const std::vector<int> hist = load<int>(dir + "/hist.bin", bs), lens = load<int>(dir + "/lens.bin", bs);
         int tokens = 0, maxq = 0, maxk = 0;
@@ -88,10 +91,16 @@ int main(int argc, char** argv) {
         Dev<float> x((size_t)tokens * H), y((size_t)tokens * H), kc(cache_n), vc(cache_n), un(H), logits(V);
         kc.put(load<float>(dir + "/kcache.bin", cache_n));
         vc.put(load<float>(dir + "/vcache.bin", cache_n));
+        Dev<half_t> kh(f16 ? cache_n : 1), vh(f16 ? cache_n : 1);
+        if (f16) {
+            LLMI_CALL(llmi_convert(kc.p, LLMI_F32, kh.p, LLMI_F16, cache_n, nullptr));
+            LLMI_CALL(llmi_convert(vc.p, LLMI_F32, vh.p, LLMI_F16, cache_n, nullptr));
+        }
         TensorWrapper<int> id_t(GPU, INT32, {tokens}, did.p), hist_t(GPU, INT32, {bs}, dhist.p),
             q_t(GPU, INT32, {bs}, dlens.p), k_t(GPU, INT32, {bs}, dctx.p);
         TensorWrapper<float> in(GPU, FP32, {tokens, H}, x.p), out(GPU, FP32, {tokens, H}, y.p);
         TensorWrapper<float> kcache(GPU, FP32, {L, bs, kv, S, hd}, kc.p), vcache(GPU, FP32, {L, bs, kv, S, hd}, vc.p);
+        TensorWrapper<half_t> kcache16(GPU, FP16, {L, bs, kv, S, hd}, kh.p), vcache16(GPU, FP16, {L, bs, kv, S, hd}, vh.p);
         TensorWrapper<float> unused(GPU, FP32, {1, H}, un.p), probs(GPU, FP32, {1, V}, logits.p);
         int layer0 = 0;
         TensorWrapper<int> layer_t(CPU, INT32, {1}, &layer0);
@@ -106,6 +115,10 @@ int main(int argc, char** argv) {
         TensorMap cin{{"decoder_input", &in}, {"history_length", &hist_t}, {"input_length", &q_t},
                       {"context_length", &k_t}, {"layer_id", &layer_t}};
         TensorMap cout{{"decoder_output", &out}, {"all_k_cache", &kcache}, {"all_v_cache", &vcache}};
+        if (f16) {
+            cout.insert("all_k_cache", &kcache16);
+            cout.insert("all_v_cache", &vcache16);
+        }
         dec.forward(cin, lw, cout, p);
         std::vector<float> all_logits;
         int row = 0;
@@ -118,6 +131,10 @@ int main(int argc, char** argv) {
             all_logits.insert(all_logits.end(), lg.begin(), lg.end());
         }
         save(dir + "/out_logits.bin", all_logits);
+        if (f16) {  // widened back for the comparison
+            LLMI_CALL(llmi_convert(kh.p, LLMI_F16, kc.p, LLMI_F32, cache_n, nullptr));
+            LLMI_CALL(llmi_convert(vh.p, LLMI_F16, vc.p, LLMI_F32, cache_n, nullptr));
+        }
         save(dir + "/out_k.bin", kc.get());
         save(dir + "/out_v.bin", vc.get());
         for (auto* w : lw) delete w;

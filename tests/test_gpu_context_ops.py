@@ -215,6 +215,25 @@ def test_strided_batch_gemm_attention_shapes_on_mfma(ops, shape, tb, dt):
     assert us < 80.0
 
 
+@pytest.mark.parametrize("scale", [1e30, 1e6, 1e-6, 1e-30])
+def test_strided_batch_gemm_fp32_range(ops, scale):
+    """fp32 operands outside fp16's range (|v| > 65504) or below its normals (< 6e-5) on
+    the MFMA path: each 32-deep K slab is scaled by a power of two before the hi/lo split
+    (context_ops.hip), so results stay finite and fp32-faithful. Rows of A and columns of
+    B span 12 decades (scale * 10^[-6, 6]) so every slab mixes magnitudes; float64 bar
+    1e-6 rel-L2 per output row."""
+    rng = np.random.default_rng(11)
+    m, n, k = 64, 48, 96
+    a = rng.standard_normal((1, 2, m, k)) * scale * 10.0 ** rng.uniform(-6, 6, (1, 2, m, 1))
+    b = rng.standard_normal((1, 2, k, n)) * 10.0 ** rng.uniform(-3, 3, (1, 2, 1, n))
+    a, b = a.astype(np.float32), b.astype(np.float32)
+    got = N(ops.launchLinearStridedBatchGemm(T(a), T(b)))
+    want = np.matmul(a.astype(np.float64), b.astype(np.float64))
+    assert np.isfinite(got).all()
+    err = np.linalg.norm(got - want, axis=-1) / np.linalg.norm(want, axis=-1)
+    assert err.max() < 1e-6, err.max()
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.float16, torch.int32, torch.int64])
 def test_tp_allreduce_single_rank(ops, dt):
     """llmi_tp_comm_create / llmi_tp_allreduce / llmi_tp_comm_destroy over RCCL with one

@@ -136,6 +136,28 @@ def test_prefill_fp8_lo_mode_f6():
     assert toks[512] == int(np.argmax(f["last_logits"]))
 
 
+def test_prefill_fp8_lo_mode_follows_weight_reload():
+    """The e4m3 weight copies of exact=2 are derived from the weights: after a reload
+    (load_synthetic with another seed) the next exact=2 prefill must use the new weights
+    (the copies were kept and the prefill was silently wrong)."""
+    cfg = preset("llama2-7b", layers=1, max_seq=160)
+    prompt = synth_prompt(2, 128, cfg.vocab)
+    with Engine(cfg) as e:
+        e.load_synthetic(5)
+        e.set_prompt(prompt)
+        e.prefill(len(prompt), exact=2)  # builds the e4m3 copies of seed 5
+        old = e.logits().copy()
+        e.load_synthetic(6)
+        out = {}
+        for mode in (2, 1):
+            e.set_prompt(prompt)
+            e.prefill(len(prompt), exact=mode)
+            out[mode] = e.logits().copy()
+    r, r_old = rel(out[2], out[1]), rel(out[2], old)
+    print(f"fp8-lo after reload vs exact: {r:.3e} (vs the old weights' logits: {r_old:.3e})")
+    assert r < 5e-4 and r_old > 0.1
+
+
 def test_prefill_fp8_lo_mode_falls_back_with_fp32_cache():
     """The fp8 lo pass needs the fp16-cache MFMA attention; with an fp32 cache exact=2
     runs the exact planes (bitwise the exact=1 result)."""

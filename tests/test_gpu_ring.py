@@ -1,0 +1,173 @@
+"""Decode mode 1, the persistent ring layer (csrc/ring.hip): per layer the attention launch
+plus ONE launch for o_proj + RMSNorm + gate_up + SiLU*up + down + the next layer's q/k/v,
+against the reference's fixtures and against decode mode 0 (five launches per layer).
+
+Bars (north star): tokens bit-exact, fp32 logits within 1e-3 rel-L2 of the reference. The
+ring's o_proj, gate_up and q/k/v sums are the launches' arithmetic bit for bit; its down
+projection is split over K by CU (a different fp32 summation order, exact int64 adds), so
+against mode 0 the logits agree to ~1e-6, not bitwise. Graph replay equals eager launches
+bitwise (every cross-CU sum is an exact integer add)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from llmi import _lib  # noqa: E402
+from llmi.engine import Engine, preset, synth_prompt  # noqa: E402
+from oracle import llama_ref as R  # noqa: E402
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+LOGIT_TOL = 1e-3
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def test_ring_f3_matches_reference():
+    """F3: 7B width, 2 layers, fp32 KV, 8-token prompt, 16 greedy tokens."""
+    f = load("f3_decode.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=64)
+    cfg.kv_dtype = _lib.F32
+    out = {}
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        for mode in (1, 0):
+            e.set_decode_mode(mode)
+            toks = e.generate(f["prompt"], len(f["tokens"]))
+            out[mode] = (toks, e.logits().copy(), e.kv_slot(1, 7), e.hidden().copy())
+    np.testing.assert_array_equal(out[1][0], f["tokens"])
+    r = rel(out[1][1], f["last_logits"])
+    r01 = rel(out[1][1], out[0][1])
+    print(f"ring f3 logits rel-L2 vs reference {r:.3e}, vs launches {r01:.3e}")
+    assert r < LOGIT_TOL and r01 < 2e-5
+    assert rel(out[1][2], out[0][2]) < 1e-5   # layer-1 K slot (from the ring's q/k/v phase)
+    assert rel(out[1][3], out[0][3]) < 2e-5
+
+
+def test_ring_graph_equals_eager_bitwise():
+    f = load("f3_decode.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=160)
+    outs = []
+    for g in (True, False):
+        with Engine(cfg) as e:
+            e.load_synthetic(int(f["seed"]))
+            e.set_decode_mode(1)
+            t = e.generate(f["prompt"], 140, use_graph=g)  # crosses two split-count boundaries
+            outs.append((t, e.logits().copy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("kv_dtype", [_lib.F32, _lib.F16])
+def test_ring_full_context_2048(kv_dtype):
+    """F7 (the bench shape at full context, 2 layers): a 2040-token prompt through the
+    decode graph, then greedy steps to position 2047 (32 split-KV chunks merged in the
+    ring's o_proj phase)."""
+    f = load("f7_longctx.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=2048)
+    cfg.kv_dtype = kv_dtype
+    n = len(f["tokens"])
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        e.set_decode_mode(1)
+        toks = e.generate(f["prompt"], n)
+        logits = e.logits()
+    exp_t, exp_l = (f["tokens"], f["last_logits"]) if kv_dtype == _lib.F32 else \
+        (f["f16kv_tokens"], f["f16kv_last_logits"])
+    np.testing.assert_array_equal(toks, exp_t)
+    r = rel(logits, exp_l)
+    print(f"ring f7 ctx 2048 kv={'f32' if kv_dtype == _lib.F32 else 'f16'}: logits rel-L2 {r:.3e}")
+    assert r < LOGIT_TOL
+
+
+def test_ring_full_7b_matches_launches_and_prefill():
+    """Llama-2-7B (32 layers, fp16 weights + KV): ring vs launches over 64 tokens (same
+    tokens, logits within the down projection's reordering), and prefill + ring decode."""
+    cfg = preset("llama2-7b", max_seq=640)
+    prompt = synth_prompt(1, 512, cfg.vocab)
+    with Engine(cfg) as e:
+        e.load_synthetic(0)
+        e.set_decode_mode(0)
+        t0 = e.generate(prompt[:8], 64)
+        l0 = e.logits().copy()
+        e.set_decode_mode(1)
+        t1 = e.generate(prompt[:8], 64)
+        l1 = e.logits().copy()
+        tp = e.generate(prompt, 16, prefill=True, exact=1)
+        e.set_decode_mode(0)
+        tq = e.generate(prompt, 16, prefill=True, exact=1)
+    np.testing.assert_array_equal(t0, t1)
+    r = rel(l1, l0)
+    print(f"full 7B ring vs launches, 64 tokens: logits rel-L2 {r:.3e}")
+    assert r < 1e-4
+    np.testing.assert_array_equal(tp, tq)
+
+
+def test_ring_sampling_matches_launches():
+    """Top-k sampling inside the ring's token graph draws the same stream."""
+    f = load("f3_decode.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=64)
+    out = {}
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        e.set_sampling(5, 123)
+        for mode in (0, 1):
+            e.set_decode_mode(mode)
+            out[mode] = e.generate(f["prompt"], 24)
+    np.testing.assert_array_equal(out[0], out[1])
+
+
+def test_ring_follows_weight_reload():
+    """The transposed W_down copies are rebuilt after load_synthetic."""
+    f = load("f3_decode.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=64)
+    cfg.kv_dtype = _lib.F32
+    with Engine(cfg) as e:
+        e.load_synthetic(99)
+        e.set_decode_mode(1)
+        e.generate(f["prompt"], 4)
+        e.load_synthetic(int(f["seed"]))
+        toks = e.generate(f["prompt"], len(f["tokens"]))
+        logits = e.logits()
+    np.testing.assert_array_equal(toks, f["tokens"])
+    assert rel(logits, f["last_logits"]) < LOGIT_TOL
+
+
+def test_ring_unsupported_shapes_raise():
+    """The tiny config (hidden 512) has no ring form: mode 1 is refused, mode 0 stays."""
+    f = load("tiny.npz")
+    with Engine(preset("tiny")) as e:
+        e.load_synthetic(int(f["seed"]))
+        with pytest.raises(_lib.LlmiError, match="ring layer"):
+            e.set_decode_mode(1)
+        toks = e.generate(f["prompt"], 4)
+    np.testing.assert_array_equal(toks, f["tokens"][:4])
+
+
+def test_ring_timing_restores_state():
+    """llmi_engine_time_kernel('ring') cycles the layers and restores the accumulators:
+    the decode continues with the same tokens as an untimed run."""
+    f = load("f3_decode.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=64)
+    outs = []
+    for timed in (False, True):
+        with Engine(cfg) as e:
+            e.load_synthetic(int(f["seed"]))
+            e.set_decode_mode(1)
+            e.set_prompt(f["prompt"])
+            e.decode(10)
+            if timed:
+                us, b = e.time_kernel("ring", 8)
+                assert us > 0 and b > 0
+            e.decode(6)
+            outs.append((e.tokens(), e.logits().copy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
