@@ -122,15 +122,22 @@ __device__ __forceinline__ int lds_ld(const int* p) {
 __device__ __forceinline__ void lds_st(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// bounded spin on an LDS word; the clock is read only once the word was seen unready
+__device__ __forceinline__ bool err_set(const int* err, int bit) {
+    return __hip_atomic_load(const_cast<int*>(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit;
+}
+// bounded spin on an LDS word; the clock is read only once the word was seen unready.
+// Once any wave of the launch (or an earlier launch) timed out, every later slow-path wait
+// gives up at once: a hand-off that cannot complete (e.g. a workgroup that never became
+// resident) costs one spin limit, not one per wait.
 template <typename F>
 __device__ __forceinline__ bool spin_until(F&& ready, int* err, int bit) {
     if (ready()) return true;
+    if (err_set(err, bit)) return false;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned n = 1;; ++n) {
         __builtin_amdgcn_s_sleep(1);
         if (ready()) return true;
-        if ((n & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit) {
+        if ((n & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(err, bit))) {
             if ((threadIdx.x & 63) == 0) atomicOr(err, bit);
             return false;
         }
@@ -273,12 +280,12 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
                 v += __shfl_xor(v, 4);
                 return __shfl(v, 0) >= (unsigned)G;
             };
-            if (!ready()) {
+            if (!ready() && !err_set(a.err, 32)) {
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 for (unsigned n = 1;; ++n) {
                     __builtin_amdgcn_s_sleep(2);
                     if (ready()) break;
-                    if ((n & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit) {
+                    if ((n & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a.err, 32))) {
                         if (lane == 0) atomicOr(a.err, 32);
                         break;
                     }
