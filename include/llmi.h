@@ -369,6 +369,11 @@ int llmi_engine_set_decode_mode(llmi_engine* e, int mode);
  *   2. the launcher all-gathers the handles (any side channel; rank order);
  *   3. llmi_engine_xchg_open(e, handles[world * 64]): map every peer's inbox;
  *   4. llmi_engine_set_exchange(e, 1) (0 = RCCL again; graphs are re-captured).
+ *      Mode 2 runs the same protocol from INSIDE the producing launches: the o_proj, down
+ *      and lm_head kernels end with an arrival ticket; their last workgroups push the
+ *      finished vector to every inbox, wait for the peers and reduce in rank order (no
+ *      exchange launch, 2 L + 1 fewer launches and kernel boundaries per token); results
+ *      are bitwise those of modes 0 and 1.
  * A peer that never arrives (2 s) sets error bit 8: llmi_engine_tokens fails, no hang. */
 int llmi_engine_xchg_handle(llmi_engine* e, void* out64);
 int llmi_engine_xchg_open(llmi_engine* e, const void* handles);
@@ -411,7 +416,9 @@ int llmi_group_logits(llmi_group* g, float* out, int n);
 int llmi_group_hidden(llmi_group* g, int rank, float* out, int n);
 /* mode 0: the in-place reduction kernel; 1: the one-shot peer exchange's kernels (every
  * rank's push, then every rank's wait + rank-order reduce; the ranks' inboxes are the
- * group's own device buffers) -- the single-GPU parity check of that protocol. */
+ * group's own device buffers) -- the single-GPU parity check of that protocol; 2: the
+ * push fused into every rank's o_proj / down / lm_head launch (their tails), then every
+ * rank's reduce kernel (one stream: an in-launch wait for a later rank cannot finish). */
 int llmi_group_set_exchange(llmi_group* g, int mode);
 
 #ifdef __cplusplus

@@ -30,6 +30,7 @@
 #include <cstdlib>
 
 #include "attn_impl.h"
+#include "xchg_impl.h"
 
 namespace llmi {
 namespace {
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(kThreads) void attn_oproj_kernel(OprojArgs a, int n
     extern __shared__ __attribute__((aligned(16))) float smem[];
     WgStamp ts(a.stamps);
     oproj_body<WT, NPL, PlainIO>(a, blockIdx.x, blockIdx.y, ns, smem);
+    xchg_detail::xchg_tail(a.xt, a.xt_cnt, reinterpret_cast<int*>(smem));  // TP: push xacc from this launch
 }
 
 int oproj_npl(const OprojArgs& a) {

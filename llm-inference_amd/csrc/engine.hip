@@ -138,8 +138,14 @@ struct Engine {
     ncclComm_t comm = nullptr;
     // one-shot peer exchange (xchg.hip): this rank's inbox (uncached HBM), every rank's
     // inbox base (IPC-mapped for peers) in device memory, per-slice epoch counters.
-    // xchg_mode 1 replaces the RCCL all-reduces of the token graph (RCCL stays selectable).
+    // xchg_mode 1 replaces the RCCL all-reduces of the token graph (RCCL stays selectable);
+    // xchg_mode 2 moves the exchange into the producing launches (o_proj, down, lm_head
+    // finish with xchg_tail: push + wait + reduce, no exchange launch). tail_mode: what
+    // those launches do (0 nothing, 1 push only -- the in-process group, 3 push + reduce);
+    // xt_cnt their arrival counter pair (zeroed here, reset by each launch's last tail).
     int xchg_mode = 0;
+    int tail_mode = 0;
+    unsigned* xt_cnt = nullptr;
     char* inbox = nullptr;
     char** peers_dev = nullptr;
     unsigned long long* xchg_ep = nullptr;
@@ -208,6 +214,7 @@ struct Engine {
         if (inbox) (void)hipFree(inbox);
         if (peers_dev) (void)hipFree(peers_dev);
         if (xchg_ep) (void)hipFree(xchg_ep);
+        if (xt_cnt) (void)hipFree(xt_cnt);
         if (wblob) (void)hipFree(wblob);
         if (kcache) (void)hipFree(kcache);
         if (vcache) (void)hipFree(vcache);
@@ -683,14 +690,29 @@ struct Engine {
     int rec_attn(int l) {
         LLMI_TRY(gemv_launch(qkv_args(l), stream));
         LLMI_TRY(attn_decode_launch(attn_args(l), stream));
-        return attn_oproj_launch(o_args(l), stream);
+        OprojArgs o = o_args(l);
+        if (tail_mode) {  // the o_proj launch pushes (and reduces) xacc itself
+            o.xt = xchg_args(xacc, c.hidden, 0, tail_mode);
+            o.xt_cnt = xt_cnt;
+        }
+        return attn_oproj_launch(o, stream);
     }
     int rec_ffn(int l) {
         LLMI_TRY(gemv_launch(gu_args(l), stream));
-        return gemv_launch(down_args(l), stream);
+        GemvArgs d = down_args(l);
+        if (tail_mode) {  // the down launch pushes (and reduces) the layer output itself
+            d.xt = xchg_args(res[(l + 1) % 2], c.hidden, 0, tail_mode);
+            d.xt_cnt = xt_cnt;
+        }
+        return gemv_launch(d, stream);
     }
     int rec_head(bool from_x = false) {
-        LLMI_TRY(gemv_launch(lm_args(from_x), stream));
+        GemvArgs h = lm_args(from_x);
+        if (tail_mode) {  // the lm_head launch max-reduces the argmax keys itself
+            h.xt = xchg_args(partials, lm_grid, 2, tail_mode);
+            h.xt_cnt = xt_cnt;
+        }
+        LLMI_TRY(gemv_launch(h, stream));
         if (sample_k == 0) return LLMI_OK;
         // top-K of this token's logits, then the sampled id replaces the argmax partials
         LLMI_TRY(topk_launch(logits, LLMI_F32, 1, c.vocab, sample_k, samp_ids, samp_vals, stream));
@@ -712,6 +734,8 @@ struct Engine {
         LLMI_HIP(hipMalloc(&xchg_ep, kXchgMaxSlices * sizeof(unsigned long long)));
         LLMI_HIP(hipMemset(xchg_ep, 0, kXchgMaxSlices * sizeof(unsigned long long)));
         LLMI_HIP(hipMalloc(&peers_dev, (size_t)W * sizeof(char*)));
+        LLMI_HIP(hipMalloc(&xt_cnt, 64));
+        LLMI_HIP(hipMemset(xt_cnt, 0, 64));
         return LLMI_OK;
     }
     // every rank's inbox base, in rank order (peers[rank] must be this rank's own inbox)
@@ -737,6 +761,7 @@ struct Engine {
     }
     int exchange(void* buf, int n, int op) {
         if (xchg_mode == 1) return xchg_launch(xchg_args(buf, n, op, 3), stream);
+        if (xchg_mode == 2) return LLMI_OK;  // the producing launch's tail did it
         if (!comm) return LLMI_OK;
         const ncclResult_t r = op == 0 ? ncclAllReduce(buf, buf, n, ncclInt64, ncclSum, comm, stream)
                                        : ncclAllReduce(buf, buf, n, ncclUint64, ncclMax, comm, stream);
@@ -744,12 +769,14 @@ struct Engine {
         return LLMI_OK;
     }
     int set_exchange(int mode) {
-        LLMI_REQUIRE(mode == 0 || mode == 1, "set_exchange: mode must be 0 (RCCL) or 1 (one-shot peer exchange)");
+        LLMI_REQUIRE(mode >= 0 && mode <= 2,
+                     "set_exchange: mode must be 0 (RCCL), 1 (one-shot peer exchange) or 2 (fused into the producers)");
         LLMI_REQUIRE(!grouped, "set_exchange: a group rank's exchange is its group's");
         LLMI_REQUIRE(mode == 0 || (inbox && peers_ready), "set_exchange: open the peer exchange first (xchg_open)");
         LLMI_HIP(hipStreamSynchronize(stream));
         graphs.clear();  // the captured steps change
         xchg_mode = mode;
+        tail_mode = mode == 2 ? 3 : 0;
         return LLMI_OK;
     }
     bool peers_ready = false;
@@ -895,7 +922,7 @@ struct Engine {
 
     int decode(int n, int use_graph) {
         LLMI_REQUIRE(prompt_len > 0, "decode: set_prompt first");
-        LLMI_REQUIRE(c.tp_world == 1 || comm || xchg_mode == 1,
+        LLMI_REQUIRE(c.tp_world == 1 || comm || xchg_mode >= 1,
                      "decode: tp_world > 1 needs an RCCL id at create or the one-shot exchange (xchg_open + set_exchange)");
         LLMI_REQUIRE(n >= 0 && host_next_pos + n <= c.max_seq, "decode: would run past max_seq");
         if (decode_mode == 1 && n > 0) LLMI_TRY(prepare_ring());
@@ -1199,7 +1226,9 @@ struct Group {
     void** ptrs = nullptr;  // device [4][W]: xacc, res[0], res[1], partials of every rank
     StepGraphs graphs;
     // 0: group_reduce_kernel; 1: the one-shot peer exchange's kernels (xchg.hip) -- every
-    // rank's push, then every rank's reduce (one stream: the waits find their flags set)
+    // rank's push, then every rank's reduce (one stream: the waits find their flags set);
+    // 2: the producer-fused form -- every rank's o_proj / down / lm_head launch pushes from
+    // its tail (tail_mode 1), then every rank's reduce kernel
     int xchg_mode = 0;
 
     ~Group() {
@@ -1233,8 +1262,9 @@ struct Group {
     }
 
     int set_exchange(int mode) {
-        LLMI_REQUIRE(mode == 0 || mode == 1, "group set_exchange: mode must be 0 (reduce kernel) or 1 (one-shot)");
-        if (mode == 1) {
+        LLMI_REQUIRE(mode >= 0 && mode <= 2,
+                     "group set_exchange: mode must be 0 (reduce kernel), 1 (one-shot) or 2 (push fused into the producers)");
+        if (mode >= 1) {
             std::vector<char*> inboxes;
             for (auto& e : r) {
                 LLMI_TRY(e->alloc_xchg());
@@ -1245,6 +1275,7 @@ struct Group {
         LLMI_HIP(hipStreamSynchronize(stream));
         graphs.clear();
         xchg_mode = mode;
+        for (auto& e : r) e->tail_mode = mode == 2 ? 1 : 0;
         return LLMI_OK;
     }
     // slot: 0 xacc, 1 res[0], 2 res[1], 3 argmax partials
@@ -1255,7 +1286,8 @@ struct Group {
         auto buf = [&](Engine& e) -> void* {
             return slot == 0 ? (void*)e.xacc : slot == 3 ? (void*)e.partials : (void*)e.res[slot - 1];
         };
-        for (auto& e : r) LLMI_TRY(xchg_launch(e->xchg_args(buf(*e), n, op, 1), stream));
+        if (xchg_mode == 1)  // (mode 2: the producers pushed already)
+            for (auto& e : r) LLMI_TRY(xchg_launch(e->xchg_args(buf(*e), n, op, 1), stream));
         for (auto& e : r) LLMI_TRY(xchg_launch(e->xchg_args(buf(*e), n, op, 2), stream));
         return LLMI_OK;
     }

@@ -3,6 +3,7 @@
 // (split so the build compiles the dtypes in parallel).
 #pragma once
 #include "gemv_impl.h"
+#include "xchg_impl.h"
 
 namespace llmi {
 namespace gemv_detail {
@@ -27,6 +28,10 @@ __global__ __launch_bounds__(kThreads, min_waves<WT>()) void gemv_kernel(GemvArg
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
     WgStamp ts(a.stamps);
     gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs);
+    if constexpr (EPI == EPI_ATOMIC || EPI == EPI_ARGMAX) {  // TP: push yacc / the argmax keys from this launch
+        const int k4 = (EPI == EPI_ATOMIC ? a.k / a.ksplit : a.k) / 4;
+        xchg_detail::xchg_tail(a.xt, a.xt_cnt, reinterpret_cast<int*>(xs + k4) + 15);  // red[15]: free by now
+    }
 }
 
 // Workgroups of one instantiation that fit the chip at once (occupancy x CUs),

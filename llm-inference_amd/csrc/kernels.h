@@ -17,6 +17,20 @@ enum GemvEpi : int {
     EPI_SLAB = 5,      // gemm2 split-K: partial [slice][m][ldy] stored; the next rows_split adds the slices in order
 };
 
+// one-shot peer exchange of a vector (xchg.hip / xchg_impl.h); also carried by the
+// producer kernels (GemvArgs / OprojArgs::xt) for the producer-fused form (buf null = off)
+struct XchgArgs {
+    long long* buf = nullptr;         // this rank's contribution in, the reduction out (n 8-B elements)
+    int n = 0;
+    int op = 0;                       // 0: int64 sum, 2: uint64 max
+    int rank = 0, world = 1;
+    char* const* peers = nullptr;     // device array [world]: every rank's inbox (peers[rank] = own)
+    unsigned long long* ep = nullptr; // [kXchgMaxSlices] epoch counters (this rank's memory)
+    int* err = nullptr;               // DecodeState::error; bit 8 = a peer never arrived (timeout)
+    int mode = 3;                     // 1: push only, 2: wait + reduce only, 3: both
+    int cap_n = 0, cap_w = 0;         // inbox geometry: elements per slot, slots per phase
+};
+
 struct GemvArgs {
     unsigned long long* stamps = nullptr;  // debug timeline (WgStamp), null = off
     const void* w = nullptr;       // [n_rows, k] row-major, dtype w_dtype
@@ -49,6 +63,10 @@ struct GemvArgs {
     long long* seed_dst = nullptr;
     int seed_n = 0;
     int seed_keep = 1;
+    // producer-fused TP exchange of the vector this launch produces (yacc / partials):
+    // xt.buf null = off; xt_cnt = the engine's arrival counter pair (xchg_impl.h xchg_tail)
+    XchgArgs xt;
+    unsigned* xt_cnt = nullptr;
 };
 
 int gemv_launch(const GemvArgs& a, hipStream_t s);
@@ -219,6 +237,8 @@ struct OprojArgs {
     const void* workspace = nullptr;  // attention partials
     long long* xacc = nullptr;
     int nact = 0;  // > 0: active split count known on the host (no position read); see AttnArgs
+    XchgArgs xt;              // producer-fused TP exchange of xacc (xt.buf null = off)
+    unsigned* xt_cnt = nullptr;
 };
 int attn_oproj_launch(const OprojArgs& a, hipStream_t s);
 
@@ -345,17 +365,6 @@ int repeat_kv_launch(const void* k_cache, const void* v_cache, int dtype, int la
 // --------------------------------------------- one-shot TP exchange (xchg.hip)
 constexpr int kXchgSlice = 256;     // vector elements per workgroup
 constexpr int kXchgMaxSlices = 64;  // n <= 16384 elements
-struct XchgArgs {
-    long long* buf = nullptr;         // this rank's contribution in, the reduction out (n 8-B elements)
-    int n = 0;
-    int op = 0;                       // 0: int64 sum, 2: uint64 max
-    int rank = 0, world = 1;
-    char* const* peers = nullptr;     // device array [world]: every rank's inbox (peers[rank] = own)
-    unsigned long long* ep = nullptr; // [kXchgMaxSlices] epoch counters (this rank's memory)
-    int* err = nullptr;               // DecodeState::error; bit 8 = a peer never arrived (timeout)
-    int mode = 3;                     // 1: push only, 2: wait + reduce only, 3: both
-    int cap_n = 0, cap_w = 0;         // inbox geometry: elements per slot, slots per phase
-};
 size_t xchg_inbox_bytes(int world, int cap_n);
 int xchg_launch(const XchgArgs& a, hipStream_t s);
 

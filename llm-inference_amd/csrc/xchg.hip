@@ -25,77 +25,18 @@
 // Liveness: every wait is bounded (kXchgTimeoutTicks of the 100 MHz clock); a timeout
 // sets bit 8 of the decode state's error word -- tokens_out raises -- and later waits
 // of the run are skipped, so a lost peer ends the run with an error instead of a hang.
-#include "kernels.h"
+#include "xchg_impl.h"
 
 namespace llmi {
 namespace {
 
 constexpr int kXThreads = kXchgSlice / 2;          // two 8-B elements (one 16-B access) per thread
-constexpr unsigned long long kXchgTimeoutTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
-
-__device__ __forceinline__ size_t data_elems(const XchgArgs& a) { return (size_t)2 * a.cap_w * a.cap_n; }
 
 __global__ __launch_bounds__(kXThreads) void xchg_kernel(XchgArgs a) {
-    const int g = blockIdx.x, tid = threadIdx.x;
-    const int i0 = g * kXchgSlice + 2 * tid;
+    const int g = blockIdx.x;
     const unsigned long long e = a.ep[g] + 1;
-    const int ph = (int)(e & 1ull);
-    auto slot = [&](char* base, int q) {
-        return reinterpret_cast<long long*>(base) + ((size_t)ph * a.cap_w + q) * a.cap_n;
-    };
-    auto flag = [&](char* base, int q) {
-        return reinterpret_cast<unsigned long long*>(reinterpret_cast<long long*>(base) + data_elems(a)) +
-               ((size_t)ph * a.cap_w + q) * kXchgMaxSlices + g;
-    };
-    if (a.mode & 1) {  // push: this rank's slice into slot [ph][rank] of every inbox
-        longlong2 v = make_longlong2(0, 0);
-        if (i0 + 1 < a.n) {
-            v = *reinterpret_cast<const longlong2*>(a.buf + i0);
-        } else if (i0 < a.n) {
-            v.x = a.buf[i0];
-        }
-        if (i0 < a.n)
-            for (int q = 0; q < a.world; ++q) *reinterpret_cast<longlong2*>(slot(a.peers[q], a.rank) + i0) = v;
-        __threadfence_system();  // every lane's data is visible system-wide ...
-        __syncthreads();         // ... before lane 0 raises the flags
-        if (tid == 0)
-            for (int q = 0; q < a.world; ++q)
-                __hip_atomic_store(flag(a.peers[q], a.rank), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (a.mode & 2) {  // wait for every rank's slice, reduce in rank order
-        char* own = a.peers[a.rank];
-        if (tid < a.world) {
-            unsigned long long* f = flag(own, tid);
-            const bool dead = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8;
-            if (!dead) {
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                for (unsigned it = 0;; ++it) {
-                    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == e) break;
-                    if ((it & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
-                        atomicOr(a.err, 8);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-        }
-        __syncthreads();
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the slots written by the peers
-        if (i0 < a.n) {
-            long long s0 = 0, s1 = 0;
-            unsigned long long m0 = 0, m1 = 0;
-            for (int q = 0; q < a.world; ++q) {
-                const longlong2 v = *reinterpret_cast<const longlong2*>(slot(own, q) + i0);
-                s0 += v.x;
-                s1 += v.y;
-                m0 = max(m0, (unsigned long long)v.x);
-                m1 = max(m1, (unsigned long long)v.y);
-            }
-            a.buf[i0] = a.op == 0 ? s0 : (long long)m0;
-            if (i0 + 1 < a.n) a.buf[i0 + 1] = a.op == 0 ? s1 : (long long)m1;
-        }
-        if (tid == 0) a.ep[g] = e;
-    }
+    if (a.mode & 1) xchg_detail::push_slice<false>(a, g, e);  // this rank's slice into every inbox
+    if (a.mode & 2) xchg_detail::reduce_slice(a, g, e);       // every rank's slice, summed in rank order
 }
 
 }  // namespace

@@ -1,0 +1,145 @@
+// Device side of the one-shot peer exchange (xchg.hip), shared by its own kernel and by
+// the producer-fused form: the o_proj / down / lm_head kernels that finish with
+// xchg_tail() push their finished vector from inside the launch (no exchange launch, no
+// extra kernel boundary per exchange). Protocol and inbox layout: xchg.hip header.
+#pragma once
+#include "kernels.h"
+
+namespace llmi {
+namespace xchg_detail {
+
+constexpr unsigned long long kTimeoutTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ size_t data_elems(const XchgArgs& a) { return (size_t)2 * a.cap_w * a.cap_n; }
+__device__ __forceinline__ long long* slot_of(const XchgArgs& a, char* base, int ph, int q) {
+    return reinterpret_cast<long long*>(base) + ((size_t)ph * a.cap_w + q) * a.cap_n;
+}
+__device__ __forceinline__ unsigned long long* flag_of(const XchgArgs& a, char* base, int ph, int q, int g) {
+    return reinterpret_cast<unsigned long long*>(reinterpret_cast<long long*>(base) + data_elems(a)) +
+           ((size_t)ph * a.cap_w + q) * kXchgMaxSlices + g;
+}
+__device__ __forceinline__ long long ld_agent(const long long* p) {
+    return (long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<long long*>(p)),
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Push slice g (elements [g * kXchgSlice, ...) of a.buf) into slot [ph][rank] of every
+// inbox, then raise flag [ph][rank][g] = e in every inbox. Block-wide (every thread calls).
+// AGENT: read buf with agent-scope loads (its values were produced inside this launch by
+// other workgroups' device-scope atomics / released stores).
+template <bool AGENT>
+__device__ __forceinline__ void push_slice(const XchgArgs& a, int g, unsigned long long e) {
+    const int ph = (int)(e & 1ull);
+    const int i_end = min(a.n, (g + 1) * kXchgSlice);
+    for (int i0 = g * kXchgSlice + 2 * (int)threadIdx.x; i0 < i_end; i0 += 2 * (int)blockDim.x) {
+        longlong2 v = make_longlong2(0, 0);
+        if constexpr (AGENT) {
+            v.x = ld_agent(a.buf + i0);
+            if (i0 + 1 < a.n) v.y = ld_agent(a.buf + i0 + 1);
+        } else if (i0 + 1 < a.n) {
+            v = *reinterpret_cast<const longlong2*>(a.buf + i0);
+        } else {
+            v.x = a.buf[i0];
+        }
+        for (int q = 0; q < a.world; ++q) *reinterpret_cast<longlong2*>(slot_of(a, a.peers[q], ph, a.rank) + i0) = v;
+    }
+    __threadfence_system();  // every lane's data is visible system-wide ...
+    __syncthreads();         // ... before one lane raises the flags
+    if (threadIdx.x == 0)
+        for (int q = 0; q < a.world; ++q)
+            __hip_atomic_store(flag_of(a, a.peers[q], ph, a.rank, g), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wait until every rank's slice g of exchange e arrived in this rank's inbox, sum (op 0) /
+// max (op 2) the W slots in rank order into a.buf, and record e as slice g's epoch.
+// Block-wide. A peer that never arrives: error bit 8 (tokens_out raises), later waits skip.
+__device__ __forceinline__ void reduce_slice(const XchgArgs& a, int g, unsigned long long e) {
+    const int ph = (int)(e & 1ull);
+    char* own = a.peers[a.rank];
+    if ((int)threadIdx.x < a.world) {
+        unsigned long long* f = flag_of(a, own, ph, threadIdx.x, g);
+        const bool dead = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8;
+        if (!dead) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (unsigned it = 0;; ++it) {
+                if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == e) break;
+                if ((it & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+                    atomicOr(a.err, 8);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    }
+    __syncthreads();
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the slots written by the peers
+    const int i_end = min(a.n, (g + 1) * kXchgSlice);
+    for (int i0 = g * kXchgSlice + 2 * (int)threadIdx.x; i0 < i_end; i0 += 2 * (int)blockDim.x) {
+        long long s0 = 0, s1 = 0;
+        unsigned long long m0 = 0, m1 = 0;
+        for (int q = 0; q < a.world; ++q) {
+            const longlong2 v = *reinterpret_cast<const longlong2*>(slot_of(a, own, ph, q) + i0);
+            s0 += v.x;
+            s1 += v.y;
+            m0 = max(m0, (unsigned long long)v.x);
+            m1 = max(m1, (unsigned long long)v.y);
+        }
+        a.buf[i0] = a.op == 0 ? s0 : (long long)m0;
+        if (i0 + 1 < a.n) a.buf[i0 + 1] = a.op == 0 ? s1 : (long long)m1;
+    }
+    if (threadIdx.x == 0) a.ep[g] = e;
+}
+
+// The producer-fused exchange: called by EVERY thread of EVERY workgroup of a kernel whose
+// workgroups produced a.buf (int64 atomics or stores), after their last write. Each
+// workgroup drains its writes, releases them (agent scope) and takes an arrival ticket;
+// the last m = min(grid, slices) to arrive wait for the grid's last arrival, then each
+// pushes (a.mode & 1) and reduces (a.mode & 2) slices j, j + m, ... The counter pair
+// cnt[0..1] (zeroed at allocation) is reset by the last tail workgroup to finish, so the
+// next fused launch on the stream finds it zero. lds: one int of LDS scratch.
+// Waits are bounded (error bit 8), so a lost peer ends the run with an error, never a hang.
+__device__ __forceinline__ void xchg_tail(const XchgArgs& a, unsigned* cnt, int* lds) {
+    if (a.buf == nullptr) return;
+    const int G = (int)(gridDim.x * gridDim.y * gridDim.z);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's atomics / stores done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *lds = (int)__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int t = *lds;
+    const int ns = (a.n + kXchgSlice - 1) / kXchgSlice;
+    const int m = min(G, ns);
+    if (t < G - m) return;
+    if (threadIdx.x == 0) {  // the grid's last arrival (the other tail workgroups are already resident)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (unsigned it = 0;; ++it) {
+            if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)G) break;
+            if ((it & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+                atomicOr(a.err, 8);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    for (int g = t - (G - m); g < ns; g += m) {
+        const unsigned long long e = a.ep[g] + 1;
+        if (a.mode & 1) push_slice<true>(a, g, e);
+        if (a.mode & 2) reduce_slice(a, g, e);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const unsigned d = __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == (unsigned)m - 1) {  // every tail workgroup is past its wait
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+}  // namespace xchg_detail
+}  // namespace llmi

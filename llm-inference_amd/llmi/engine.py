@@ -151,7 +151,8 @@ class Engine:
         call("llmi_engine_xchg_open", self._h, buf)
 
     def set_exchange(self, mode: int):
-        """0: RCCL all-reduces (needs a tp_id at create); 1: the one-shot peer exchange."""
+        """0: RCCL all-reduces (needs a tp_id at create); 1: the one-shot peer exchange;
+        2: the same exchange fused into the producing launches (o_proj / down / lm_head)."""
         call("llmi_engine_set_exchange", self._h, int(mode))
 
     def set_decode_mode(self, mode: int):
@@ -231,7 +232,8 @@ class TPGroup:
         return out
 
     def set_exchange(self, mode: int):
-        """0: in-place reduction kernel; 1: the one-shot peer exchange kernels."""
+        """0: in-place reduction kernel; 1: the one-shot peer exchange kernels; 2: the push
+        fused into every rank's producing launches, then the reduce kernels."""
         call("llmi_group_set_exchange", self._h, int(mode))
 
     def generate(self, prompt, n_new: int, use_graph: bool = True) -> np.ndarray:

@@ -45,14 +45,27 @@ def main():
         paths = [os.path.join(rdv, f"h{q}") for q in range(world)]
         wait_for(paths)
         e.xchg_open([open(p, "rb").read() for p in paths])
-        e.set_exchange(1)
+        mode = int(os.environ.get("XCHG_MODE", "1"))  # 1: exchange launches, 2: fused into the producers
+        e.set_exchange(mode)
         toks = {}
         for g in (True, False):
             toks[g] = e.generate(f["prompt"], n_new, use_graph=g)
         logits = e.logits()
         timing = {}
         if os.environ.get("XCHG_TIME"):  # a collective: every rank times the same calls
+            e.set_exchange(1)
             timing = {k: e.time_kernel(k, 256)[0] for k in ("xchg", "xchg_graph")}
+            n_loop = min(cfg.max_seq - 1, 48)
+            for m in (1, 2, 1, 2):  # graph-replayed decode per exchange form, alternating
+                e.set_exchange(m)
+                e.generate(f["prompt"], 4)  # capture + warm
+                e.set_prompt(f["prompt"])
+                e.sync()
+                t0 = time.perf_counter()
+                e.decode(n_loop)
+                e.sync()
+                us = (time.perf_counter() - t0) / n_loop * 1e6
+                timing[f"loop_mode{m}"] = min(us, timing.get(f"loop_mode{m}", us))
         np.savez(os.path.join(rdv, f"out_{rank}.npz"), tokens=toks[True], tokens_eager=toks[False], logits=logits,
                  **{f"us_{k}": np.float64(v) for k, v in timing.items()})
         # stay alive until every rank is done (no inbox freed while a peer may still write it)

@@ -41,16 +41,19 @@ def group_run(name, cfg, world, mode, use_graph):
         return f, toks, per_rank, g.logits(), [g.hidden(r) for r in range(world)]
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("name,pname,kw,world,use_graph", [
     ("tiny.npz", "tiny", {}, 2, True),
     ("tiny.npz", "tiny", {}, 4, False),
     ("f4_tp8.npz", "llama2-7b", {"layers": 2, "max_seq": 64}, 8, True),
 ])
-def test_group_oneshot_equals_reduce_kernel_bitwise(name, pname, kw, world, use_graph):
+def test_group_oneshot_equals_reduce_kernel_bitwise(name, pname, kw, world, use_graph, mode):
+    """mode 1: exchange launches; mode 2: the push fused into the o_proj / down / lm_head
+    launches (their tails), then the reduce kernels."""
     cfg = preset(pname, **kw)
     cfg.kv_dtype = _lib.F32
     f, t0, r0, l0, h0 = group_run(name, cfg, world, 0, use_graph)
-    _, t1, r1, l1, h1 = group_run(name, cfg, world, 1, use_graph)
+    _, t1, r1, l1, h1 = group_run(name, cfg, world, mode, use_graph)
     np.testing.assert_array_equal(t1, f["tokens"])
     np.testing.assert_array_equal(t1, t0)
     for a, b in zip(r1, r0):
@@ -60,14 +63,19 @@ def test_group_oneshot_equals_reduce_kernel_bitwise(name, pname, kw, world, use_
         np.testing.assert_array_equal(a, b)
 
 
-def test_oneshot_two_processes_one_gpu_ipc(tmp_path):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_oneshot_two_processes_one_gpu_ipc(tmp_path, mode):
     """Two rank processes on device 0 (RCCL refuses that; the one-shot exchange does not
-    care where the peer's inbox lives): IPC handles through files, cross-process flags."""
+    care where the peer's inbox lives): IPC handles through files, cross-process flags.
+    mode 2: each process's o_proj / down / lm_head launches push, wait for the other
+    process and reduce from inside the launch."""
     f = load("tiny.npz")
     n_new = len(f["tokens"])
     worker = os.path.join(HERE, "helpers", "xchg_worker.py")
+    env = dict(os.environ, XCHG_MODE=str(mode))
     procs = [subprocess.Popen([sys.executable, worker, str(r), "2", "0", str(tmp_path), os.path.join(G, "tiny.npz"),
-                               "tiny", str(n_new)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                               "tiny", str(n_new)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                              env=env)
              for r in range(2)]
     outs = []
     try:
