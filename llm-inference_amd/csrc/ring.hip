@@ -55,6 +55,9 @@ constexpr int kXOff = kSlots * kPiece;      // fp32 x image [kH]
 constexpr int kCtl = kXOff + kH * 4;        // control words, act, merged head, scratch
 constexpr int kLds = kCtl + 4096;
 constexpr unsigned long long kSpinLimit = 20000000ull;  // 200 ms of the 100 MHz clock
+#ifndef LLMI_RING_PROF
+#define LLMI_RING_PROF 0  // 1: the 8 stamp words of a workgroup hold wait-time totals instead (tools/ring_timeline.py --prof)
+#endif
 
 struct Plan {
     int h, r0, s_o;     // O: head, first W_o row, pieces (32 rows each)
@@ -86,22 +89,27 @@ __device__ __forceinline__ Plan make_plan(const RingArgs& a, int b, int g) {
 __device__ __forceinline__ int cons_of(const Plan& p, int seq) {
     return (seq < p.b_g || (seq >= p.b_d && seq < p.b_q)) ? kCons : 1;
 }
-// lane's 16-B source of piece seq, DMA instruction j (8 per piece, 1 KB each)
-__device__ __forceinline__ const char* piece_src(const RingArgs& a, const Plan& p, int seq, int j, int lane) {
-    const int off = j * 1024 + lane * 16;
+// lane's 16-B source of piece seq for its first DMA instruction, and the byte step to
+// each of the next seven (8 per piece, 1 KB each): computed once per piece, so the
+// loader spends two VALU ops per DMA instead of re-deriving the phase and row
+__device__ __forceinline__ const char* piece_base(const RingArgs& a, const Plan& p, int seq, int lane, size_t& step) {
     if (seq < p.b_g) {  // 32 rows x 256 B of W_o: row p.r0 + 32 seq + 4 j + lane / 16, head p.h
-        const int row = p.r0 + seq * 32 + j * 4 + (lane >> 4);
+        const int row = p.r0 + seq * 32 + (lane >> 4);
+        step = (size_t)4 * a.heads * 128 * 2;
         return reinterpret_cast<const char*>(a.w_o) +
                ((size_t)row * (a.heads * 128) + (size_t)p.h * 128 + (lane & 15) * 8) * 2;
     }
+    step = 1024;
+    const char* row;
     if (seq < p.b_d) {
         const int k = seq - p.b_g;
-        const int row = ((k & 1) ? a.inter : 0) + p.p0 + (k >> 1);
-        return reinterpret_cast<const char*>(a.w_gu) + (size_t)row * kPiece + off;
+        row = reinterpret_cast<const char*>(a.w_gu) + (size_t)(((k & 1) ? a.inter : 0) + p.p0 + (k >> 1)) * kPiece;
+    } else if (seq < p.b_q) {
+        row = reinterpret_cast<const char*>(a.w_dt) + (size_t)(p.p0 + seq - p.b_d) * kPiece;
+    } else {
+        row = reinterpret_cast<const char*>(a.w_qkv) + (size_t)(p.q0 + seq - p.b_q) * kPiece;
     }
-    if (seq < p.b_q)
-        return reinterpret_cast<const char*>(a.w_dt) + (size_t)(p.p0 + seq - p.b_d) * kPiece + off;
-    return reinterpret_cast<const char*>(a.w_qkv) + (size_t)(p.q0 + seq - p.b_q) * kPiece + off;
+    return row + lane * 16;
 }
 
 __device__ __forceinline__ void glds16_nt(const void* gsrc, unsigned lds_dst) {
@@ -188,8 +196,13 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     const Plan p = make_plan(a, b, G);
     unsigned long long* ts = a.stamps ? a.stamps + 8 * (size_t)b : nullptr;
     auto stamp = [&](int i) {
-        if (ts && lane == 0) ts[i] = __builtin_amdgcn_s_memrealtime();
+        if (!LLMI_RING_PROF && ts && lane == 0) ts[i] = __builtin_amdgcn_s_memrealtime();
     };
+    // LLMI_RING_PROF: 100 MHz ticks a wave spent waiting, [2 lw] loader lw on a free slot,
+    // [2 lw + 1] loader lw on its oldest piece landing, [4 + phase] consumer wave 0 on a
+    // piece landing in phase O / G / D / Q
+    unsigned long long t_a = 0, t_b = 0, t_c = 0, t_cur = 0;
+    auto now = [&]() { return LLMI_RING_PROF ? __builtin_amdgcn_s_memrealtime() : 0ull; };
     if (tid < kSlots) {
         full[tid] = -1;
         freec[tid] = 0;
@@ -208,6 +221,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         const unsigned ring = (unsigned)(uintptr_t)smem;
         int inflight = 0, pub = lw;
         auto publish_oldest = [&]() {
+            const unsigned long long q0 = now();
             switch (inflight) {  // vmcnt needs an immediate: the oldest piece has landed
                 case 1: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
                 case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
@@ -216,6 +230,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
                 case 5: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
                 default: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
             }
+            t_b += now() - q0;
             if (lane == 0) lds_st(full + pub % kSlots, pub);
             pub += kLoaders;
             --inflight;
@@ -226,19 +241,27 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
                 const int want = lds_ld(expect + slot);
                 bool ok = true;
                 if (lds_ld(freec + slot) < want) {
+                    const unsigned long long q0 = now();
                     while (inflight > 0 && lds_ld(freec + slot) < want) publish_oldest();
                     ok = spin_until([&]() { return lds_ld(freec + slot) >= want; }, a.err, 32);
+                    t_a += now() - q0;
                 }
                 if (!ok) break;
             }
             if (lane == 0) lds_st(expect + slot, lds_ld(expect + slot) + cons_of(p, seq));
             const unsigned dst = __builtin_amdgcn_readfirstlane(ring + slot * kPiece);
+            size_t step;
+            const char* src = piece_base(a, p, seq, lane, step);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) glds16_nt(piece_src(a, p, seq, j, lane), dst + j * 1024);
+            for (int j = 0; j < 8; ++j) glds16_nt(src + j * step, dst + j * 1024);
             if (++inflight == kDepth) publish_oldest();
         }
         while (inflight > 0) publish_oldest();
         if (tid == 0) stamp(7);
+        if (LLMI_RING_PROF && ts && lane == 0) {
+            ts[2 * lw] = t_a;
+            ts[2 * lw + 1] = t_b;
+        }
         return;
     }
 
@@ -254,7 +277,13 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     };
     auto wait_full = [&](int seq) {
         const int slot = seq % kSlots;
-        spin_until([&]() { return lds_ld(full + slot) == seq; }, a.err, 32);
+        if (LLMI_RING_PROF && lds_ld(full + slot) != seq) {
+            const unsigned long long q0 = now();
+            spin_until([&]() { return lds_ld(full + slot) == seq; }, a.err, 32);
+            t_cur += now() - q0;
+        } else {
+            spin_until([&]() { return lds_ld(full + slot) == seq; }, a.err, 32);
+        }
         return smem + slot * kPiece;
     };
     auto release = [&](int seq) {  // after this wave's reads of the slot completed
@@ -438,6 +467,8 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     }
     arrive(a.cnt);
     cstamp(1);
+    t_a = t_cur;
+    t_cur = 0;
 
     // ---- G: xmid from every CU; this CU's gate/up pairs; SiLU * up into act_s
     wait_all(a.cnt);
@@ -452,6 +483,8 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     }
     cbarrier();
     cstamp(3);
+    t_b = t_cur;
+    t_cur = 0;
 
     // ---- D: x_{l+1} += W_d[:, slice] . act[slice] (this CU's rows of W_d^T); every
     // consumer thread owns 16 outputs: elements 8 ct + [0, 8) and 8 (ct + 256) + [0, 8)
@@ -490,8 +523,19 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     }
     arrive(a.cnt + kRingShards * kRingShardWords);
     cstamp(4);
+    t_c = t_cur;
+    t_cur = 0;
+    auto prof_out = [&]() {
+        if (LLMI_RING_PROF && ts && cw == 0 && lane == 0) {
+            ts[4] = t_a;
+            ts[5] = t_b;
+            ts[6] = t_c;
+            ts[7] = t_cur;
+        }
+    };
     if (!a.w_qkv) {
         cstamp(6);
+        prof_out();
         return;
     }
 
@@ -505,6 +549,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         if (lane == 0) a.qkv_out[p.q0 + r] = v;
     }
     cstamp(6);
+    prof_out();
 }
 
 // W [rows][cols] -> W^T [cols][rows], fp16, 64 x 64 tiles through LDS

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--max-seq", type=int, default=2048)
+    ap.add_argument("--prof", action="store_true",
+                    help="the library was built with -DLLMI_RING_PROF=1 (LLMI_LIB_PATH): report wait totals")
     a = ap.parse_args()
     cfg = preset("llama2-7b", layers=a.layers, max_seq=a.max_seq)
     cfg.kv_dtype = llmi.F16
@@ -68,6 +70,10 @@ def main():
                 spans.append(("qkv" if s == 0 else "lm_head" if s == n_slots - 1 else "attn", v[:, 0].min(),
                               v[:, 3].max()))
             continue
+        if a.prof:  # wait totals per workgroup (ticks), mean over workgroups and layers
+            v = rows[:256]
+            phase.append(v.mean(axis=0))
+            continue
         v = rows[rows[:, 0] > 0]
         if not len(v):
             continue
@@ -79,6 +85,13 @@ def main():
             col = col[col > 0] - t0
             marks.append([float(np.min(col)), float(np.median(col)), float(np.max(col))] if len(col) else [0, 0, 0])
         phase.append(marks)
+    if a.prof:
+        m = np.array(phase).mean(axis=0) / 100.0
+        names = ["loader0_free_wait", "loader0_land_wait", "loader1_free_wait", "loader1_land_wait",
+                 "cons0_full_wait_O", "cons0_full_wait_G", "cons0_full_wait_D", "cons0_full_wait_Q"]
+        print(json.dumps({"ctx": a.ctx, "layers": a.layers, "prof_us_mean_per_wg": {k: round(float(x), 2)
+                                                                                    for k, x in zip(names, m)}}))
+        return
     ph = np.array(phase) / 100.0  # us
     mean = ph.mean(axis=0)
     out = {"ctx": a.ctx, "layers": a.layers, "ring_launches": len(phase),
