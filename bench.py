@@ -272,6 +272,8 @@ def open_oneshot_exchange(eng, dist, prompt, world, n_check: int = 64, rccl: boo
         ok = False
     if all(o[0] for o in oks) and (rccl or all(o[2] == oks[0][2] for o in oks)):
         info["mode"] = "oneshot"
+        fused = pick_fused_exchange(eng, dist, prompt, world, tb)
+        info.update(fused)
     elif not rccl:
         raise RuntimeError(f"one-device rehearsal: one-shot exchange failed: {[o[1] for o in oks]}")
     else:
@@ -281,6 +283,52 @@ def open_oneshot_exchange(eng, dist, prompt, world, n_check: int = 64, rccl: boo
             pass
         info["oneshot_rejected"] = [o[1] for o in oks if not o[0]][:2]
     return info
+
+
+def pick_fused_exchange(eng, dist, prompt, world, ref_tokens, n_time: int = 128):
+    """Exchange mode 2 (the push / wait / reduce fused into the o_proj, down and lm_head
+    launches) against mode 1 (one exchange launch each): both must give the tokens the
+    checked mode-1 run gave on every rank; then each is timed over n_time graph-replayed
+    forwards on every rank (a collective) and the faster by the slowest rank carries the
+    timed run. Any error keeps mode 1, with the reason."""
+    import time as _t
+    out = {}
+    ok, why = False, ""
+    try:
+        eng.set_exchange(2)
+        t2 = eng.generate(prompt, len(ref_tokens)) if ref_tokens is not None else None
+        ok = t2 is not None and bool((t2 == ref_tokens).all())
+        why = "" if ok else "fused-exchange tokens differ"
+    except Exception as e:
+        why = repr(e)[:300]
+    oks = [None] * world
+    dist.all_gather_object(oks, (ok, why))
+    if not all(o[0] for o in oks):
+        eng.set_exchange(1)
+        out["fused_rejected"] = [o[1] for o in oks if not o[0]][:2]
+        return out
+    times = {}
+    n = min(n_time, eng.cfg.max_seq - 1)
+    for m in (1, 2, 1, 2):
+        eng.set_exchange(m)
+        eng.set_prompt(prompt)
+        eng.decode(n)  # graph capture + warm
+        eng.sync()
+        eng.set_prompt(prompt)
+        dist.barrier()
+        t0 = _t.perf_counter()
+        eng.decode(n)
+        eng.sync()
+        dt = _t.perf_counter() - t0
+        times[m] = min(dt, times.get(m, dt))
+    allt = [None] * world
+    dist.all_gather_object(allt, times)
+    worst = {m: max(t[m] for t in allt) for m in (1, 2)}
+    best = 2 if worst[2] < worst[1] else 1
+    eng.set_exchange(best)
+    out["mode"] = "fused" if best == 2 else "oneshot"
+    out["us_per_forward_oneshot_vs_fused"] = [round(worst[1] / n * 1e6, 2), round(worst[2] / n * 1e6, 2)]
+    return out
 
 
 def tp_exchange_side(eng, layers, ms_per_token, wbytes, mode="rccl", rccl=True):
@@ -297,7 +345,7 @@ def tp_exchange_side(eng, layers, ms_per_token, wbytes, mode="rccl", rccl=True):
         out["allreduce_us_eager"] = round(eng.time_kernel("allreduce", iters=200)[0], 2)
         out["allreduce_us_graph"] = round(eng.time_kernel("allreduce_graph", iters=256)[0], 2)
         lat = out["allreduce_us_graph"]
-    if mode == "oneshot":
+    if mode in ("oneshot", "fused"):
         out["oneshot_us_eager"] = round(eng.time_kernel("xchg", iters=200)[0], 2)
         out["oneshot_us_graph"] = round(eng.time_kernel("xchg_graph", iters=256)[0], 2)
         lat = out["oneshot_us_graph"]
@@ -475,8 +523,9 @@ def main():
                                                    mode=xchg["mode"], rccl=tp_id is not None)
             if one_dev:
                 side["tp_exchange"]["one_device_rehearsal"] = True
-            if "oneshot_rejected" in xchg:
-                side["tp_exchange"]["oneshot_rejected"] = xchg["oneshot_rejected"]
+            for k in ("oneshot_rejected", "fused_rejected", "us_per_forward_oneshot_vs_fused"):
+                if k in xchg:
+                    side["tp_exchange"][k] = xchg[k]
         except Exception as e:  # reported, never fatal to the GPU number
             side["tp_exchange"] = {"error": repr(e)[:300]}
     if world == 1 and not args.no_side and not args.eager:

@@ -47,7 +47,14 @@ constexpr int kLoaders = 2;
 constexpr int kCons = 4;
 constexpr int kThreads = 64 * (kLoaders + kCons);
 constexpr int kCT = 64 * kCons;             // consumer threads
-constexpr int kDepth = 6;                   // pieces in flight per loader (8 DMA each: vmcnt <= 48)
+#ifndef LLMI_RING_EXP
+#define LLMI_RING_EXP 0
+#endif
+#ifndef LLMI_RING_DEPTH
+#define LLMI_RING_DEPTH 6
+#endif
+constexpr int kDepth = LLMI_RING_DEPTH;     // pieces in flight per loader (8 DMA each: vmcnt <= 48)
+static_assert(kDepth >= 1 && kDepth <= 7, "vmcnt holds at most 63 DMAs per loader wave");
 constexpr int kMaxPairs = 64;               // gate/up pairs (= W_d^T rows) per CU
 constexpr int kChunks = kH * 2 / 16;        // 16-B chunks per row (512)
 constexpr int kRowPL = kChunks / 64;        // chunks of a row per lane when one wave reads it (8)
@@ -85,9 +92,9 @@ __device__ __forceinline__ Plan make_plan(const RingArgs& a, int b, int g) {
     p.n = p.b_q + p.nq;
     return p;
 }
-// consumer waves that read piece seq (O and D: all of them, G and Q: its owner)
+// consumer waves that read piece seq (D: all of them, O, G and Q: its owner)
 __device__ __forceinline__ int cons_of(const Plan& p, int seq) {
-    return (seq < p.b_g || (seq >= p.b_d && seq < p.b_q)) ? kCons : 1;
+    return (seq >= p.b_d && seq < p.b_q) ? kCons : 1;
 }
 // lane's 16-B source of piece seq for its first DMA instruction, and the byte step to
 // each of the next seven (8 per piece, 1 KB each): computed once per piece, so the
@@ -198,17 +205,25 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     auto stamp = [&](int i) {
         if (!LLMI_RING_PROF && ts && lane == 0) ts[i] = __builtin_amdgcn_s_memrealtime();
     };
+    // LLMI_RING_PROF 2: consumer wave 0's marks through the O phase and the first seam
+    auto ostamp = [&](int i) {
+        if (LLMI_RING_PROF == 2 && ts && wave == kLoaders && lane == 0) ts[i] = __builtin_amdgcn_s_memrealtime();
+    };
     // LLMI_RING_PROF: 100 MHz ticks a wave spent waiting, [2 lw] loader lw on a free slot,
     // [2 lw + 1] loader lw on its oldest piece landing, [4 + phase] consumer wave 0 on a
     // piece landing in phase O / G / D / Q
     unsigned long long t_a = 0, t_b = 0, t_c = 0, t_cur = 0;
-    auto now = [&]() { return LLMI_RING_PROF ? __builtin_amdgcn_s_memrealtime() : 0ull; };
+    auto now = [&]() { return LLMI_RING_PROF == 1 ? __builtin_amdgcn_s_memrealtime() : 0ull; };
     if (tid < kSlots) {
         full[tid] = -1;
         freec[tid] = 0;
         expect[tid] = 0;
     }
-    if (tid == 0) *cbar = 0;
+    if (tid == 0) {
+        cbar[0] = 0;
+        cbar[1] = 0;  // G: next gate/up pair to take
+        cbar[2] = 0;  // Q: next q/k/v row to take
+    }
     __syncthreads();  // the only full-workgroup barrier: loaders never join another one
 
     if (wave < kLoaders) {
@@ -228,7 +243,8 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
                 case 3: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
                 case 4: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
                 case 5: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-                default: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+                case 6: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+                default: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
             }
             t_b += now() - q0;
             if (lane == 0) lds_st(full + pub % kSlots, pub);
@@ -258,7 +274,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         }
         while (inflight > 0) publish_oldest();
         if (tid == 0) stamp(7);
-        if (LLMI_RING_PROF && ts && lane == 0) {
+        if (LLMI_RING_PROF == 1 && ts && lane == 0) {
             ts[2 * lw] = t_a;
             ts[2 * lw + 1] = t_b;
         }
@@ -277,7 +293,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     };
     auto wait_full = [&](int seq) {
         const int slot = seq % kSlots;
-        if (LLMI_RING_PROF && lds_ld(full + slot) != seq) {
+        if (LLMI_RING_PROF == 1 && lds_ld(full + slot) != seq) {
             const unsigned long long q0 = now();
             spin_until([&]() { return lds_ld(full + slot) == seq; }, a.err, 32);
             t_cur += now() - q0;
@@ -398,6 +414,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     auto cstamp = [&](int i) {
         if (cw == 0) stamp(i);
     };
+    ostamp(0);
     // ---- housekeeping for the next launches (their accumulators / counters), and the
     // residual seed of the o_proj sum: acc_mid[slice] += x_l[slice]
     for (int i = e0 + ct; i < e0 + en; i += kCT) {
@@ -418,19 +435,31 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         const float* oh = ws.o + (size_t)p.h * ns * attn_detail::D + d;
         constexpr int kOv = 16;
         float ov[kOv];
+        // one round trip: the partial outputs and every split's (m, l), all issued together
 #pragma unroll
         for (int i = 0; i < kOv; ++i) {
             const int s = half + 2 * i;
             ov[i] = oh[(size_t)(s < nact ? s : 0) * attn_detail::D];
         }
-        float M = -INFINITY;
-        for (int s = lane; s < nact; s += 64) M = fmaxf(M, mlh[2 * s]);
+        const float2* ml2 = reinterpret_cast<const float2*>(mlh);
+        const float2 ml0 = ml2[lane < nact ? lane : 0];  // splits 0..63 (max_seq <= 4096: all of them)
+        float M = lane < nact ? ml0.x : -INFINITY;
+        for (int s = lane + 64; s < nact; s += 64) M = fmaxf(M, ml2[s].x);
         M = wave_max(M);  // every wave the same
-        for (int s = ct; s < nact; s += kCT) wm_s[s] = expf(mlh[2 * s] - M);
-        cbarrier();
+        ostamp(1);
         float L = 0.f;
-        for (int s = lane; s < nact; s += 64) L = fmaf(mlh[2 * s + 1], wm_s[s], L);
+        if (lane < nact) {
+            const float w = expf(ml0.x - M);
+            L = ml0.y * w;
+            if (cw == 0) wm_s[lane] = w;
+        }
+        for (int s = lane + 64; s < nact; s += 64) {
+            const float w = expf(ml2[s].x - M);
+            L = fmaf(ml2[s].y, w, L);
+            if (cw == 0) wm_s[s] = w;
+        }
         L = wave_sum(L);
+        cbarrier();
         float O = 0.f;
 #pragma unroll
         for (int i = 0; i < kOv; ++i) {
@@ -442,41 +471,58 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         cbarrier();
         if (!half) oh_s[d] = (O + ximg[d]) * (1.0f / L);  // attn_oproj_kernel's arithmetic, bit for bit
         cbarrier();
+        ostamp(2);
     }
     {
-        const int c16 = ct & 15, r16 = ct >> 4;  // chunk of the 128-dim head row, row of 16
-        float4 x0 = reinterpret_cast<const float4*>(oh_s)[2 * c16], x1 = reinterpret_cast<const float4*>(oh_s)[2 * c16 + 1];
-        for (int k = 0; k < p.s_o; ++k) {
+        // a whole 32-row piece per consumer wave: lane reads chunk (lane & 15) of rows
+        // lane / 16 + 4 i (i < 8), the 16 lanes of a row group reduce by xor shuffles
+        const int c16 = lane & 15, g4 = lane >> 4;
+        const float4 x0 = reinterpret_cast<const float4*>(oh_s)[2 * c16];
+        const float4 x1 = reinterpret_cast<const float4*>(oh_s)[2 * c16 + 1];
+        for (int k = cw; k < p.s_o; k += kCons) {
             const char* sp = wait_full(k);
-            const uint4 w0 = *reinterpret_cast<const uint4*>(sp + (r16 * 16 + c16) * 16);
-            const uint4 w1 = *reinterpret_cast<const uint4*>(sp + ((r16 + 16) * 16 + c16) * 16);
-            release(k);
-            float v0 = dot8(w0, x0, x1), v1 = dot8(w1, x0, x1);
+            uint4 w[8];
 #pragma unroll
-            for (int off = 8; off > 0; off >>= 1) {
-                v0 += __shfl_xor(v0, off);
-                v1 += __shfl_xor(v1, off);
-            }
-            if (c16 == 0) {  // the row sums wait in the x image (free until the gather)
-                ximg[k * 32 + r16] = v0;
-                ximg[k * 32 + r16 + 16] = v1;
-            }
+            for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const uint4*>(sp + (lane + 64 * i) * 16);
+            release(k);
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = dot8(w[i], x0, x1);
+#pragma unroll
+            for (int off = 8; off > 0; off >>= 1)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] += __shfl_xor(v[i], off);
+            if (c16 == 0)  // the row sums wait in the x image (free until the gather)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) ximg[k * 32 + g4 + 4 * i] = v[i];
         }
+        ostamp(3);
         cbarrier();  // then one wave instruction adds 64 consecutive rows (512 contiguous bytes)
         for (int i = ct; i < p.s_o * 32; i += kCT) add_fixed(a.acc_mid + p.r0 + i, ximg[i]);
+        ostamp(4);
     }
     arrive(a.cnt);
+    ostamp(5);
     cstamp(1);
     t_a = t_cur;
     t_cur = 0;
 
     // ---- G: xmid from every CU; this CU's gate/up pairs; SiLU * up into act_s
     wait_all(a.cnt);
+    ostamp(6);
     cstamp(2);
     float rstd = gather(a.acc_mid, a.acc_out);  // + seeds acc_out[slice] with xmid (the down sum adds to it)
+    ostamp(7);
     if (a.w_qkv) load_gamma(a.g_attn);
     image_to_regs();
-    for (int j = cw; j < p.np; j += kCons) {
+    // pairs are taken in ring order by whichever consumer wave is free (an LDS ticket), so
+    // one slow wave never holds the ring's oldest slots while the others starve
+    auto take = [&](int* ctr) {
+        int j = 0;
+        if (lane == 0) j = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __shfl(j, 0);
+    };
+    for (int j = take(cbar + 1); j < p.np; j = take(cbar + 1)) {
         const float g = dot_row(p.b_g + 2 * j) * rstd;
         const float u = dot_row(p.b_g + 2 * j + 1) * rstd;
         if (lane == 0) act_s[j] = silu(g) * u;
@@ -492,23 +538,43 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         float acc[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-        for (int k = 0; k < p.np; ++k) {
-            const char* sp = wait_full(p.b_d + k);
-            const uint4 w0 = *reinterpret_cast<const uint4*>(sp + ct * 16);
-            const uint4 w1 = *reinterpret_cast<const uint4*>(sp + (ct + kCT) * 16);
-            release(p.b_d + k);
-            const float av = act_s[k];
-            const __half2* h0 = reinterpret_cast<const __half2*>(&w0);
-            const __half2* h1 = reinterpret_cast<const __half2*>(&w1);
+        // kDB pieces per step: their FULL polls, LDS reads and FREE counts overlap, so the
+        // per-piece LDS round trips are paid once per step
+        constexpr int kDB = 4;
+        auto dstep = [&](int k0, int nb) {
+            uint4 w0[kDB], w1[kDB];
+            float av[kDB];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float2 f0 = __half22float2(h0[i]), f1 = __half22float2(h1[i]);
-                acc[2 * i] = fmaf(av, f0.x, acc[2 * i]);
-                acc[2 * i + 1] = fmaf(av, f0.y, acc[2 * i + 1]);
-                acc[8 + 2 * i] = fmaf(av, f1.x, acc[8 + 2 * i]);
-                acc[8 + 2 * i + 1] = fmaf(av, f1.y, acc[8 + 2 * i + 1]);
+            for (int q = 0; q < kDB; ++q) {
+                if (q < nb) {
+                    const char* sp = wait_full(p.b_d + k0 + q);
+                    w0[q] = *reinterpret_cast<const uint4*>(sp + ct * 16);
+                    w1[q] = *reinterpret_cast<const uint4*>(sp + (ct + kCT) * 16);
+                    av[q] = act_s[k0 + q];
+                }
             }
-        }
+#pragma unroll
+            for (int q = 0; q < kDB; ++q)
+                if (q < nb) release(p.b_d + k0 + q);
+#pragma unroll
+            for (int q = 0; q < kDB; ++q) {
+                if (q < nb) {
+                    const __half2* h0 = reinterpret_cast<const __half2*>(&w0[q]);
+                    const __half2* h1 = reinterpret_cast<const __half2*>(&w1[q]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float2 f0 = __half22float2(h0[i]), f1 = __half22float2(h1[i]);
+                        acc[2 * i] = fmaf(av[q], f0.x, acc[2 * i]);
+                        acc[2 * i + 1] = fmaf(av[q], f0.y, acc[2 * i + 1]);
+                        acc[8 + 2 * i] = fmaf(av[q], f1.x, acc[8 + 2 * i]);
+                        acc[8 + 2 * i + 1] = fmaf(av[q], f1.y, acc[8 + 2 * i + 1]);
+                    }
+                }
+            }
+        };
+        int k = 0;
+        for (; k + kDB <= p.np; k += kDB) dstep(k, kDB);
+        if (k < p.np) dstep(k, p.np - k);
         // through the (now free) x image, so that one wave's atomics cover 64 consecutive
         // int64 words: 512 contiguous bytes per instruction instead of 64 lanes each in its
         // own 64-B line (the scattered shape runs ~17x below the chip's atomic rate)
@@ -518,15 +584,17 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
         st[2 * (ct + kCT)] = make_float4(acc[8], acc[9], acc[10], acc[11]);
         st[2 * (ct + kCT) + 1] = make_float4(acc[12], acc[13], acc[14], acc[15]);
         cbarrier();
+#if LLMI_RING_EXP != 1  // EXP 1 (timing only, wrong output): no down atomics
 #pragma unroll
         for (int j = 0; j < kH / kCT; ++j) add_fixed(a.acc_out + j * kCT + ct, ximg[j * kCT + ct]);
+#endif
     }
     arrive(a.cnt + kRingShards * kRingShardWords);
     cstamp(4);
     t_c = t_cur;
     t_cur = 0;
     auto prof_out = [&]() {
-        if (LLMI_RING_PROF && ts && cw == 0 && lane == 0) {
+        if (LLMI_RING_PROF == 1 && ts && cw == 0 && lane == 0) {
             ts[4] = t_a;
             ts[5] = t_b;
             ts[6] = t_c;
@@ -544,7 +612,7 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     cstamp(5);
     rstd = gather(a.acc_out, nullptr);
     image_to_regs();
-    for (int r = cw; r < p.nq; r += kCons) {
+    for (int r = take(cbar + 2); r < p.nq; r = take(cbar + 2)) {
         const float v = dot_row(p.b_q + r) * rstd;
         if (lane == 0) a.qkv_out[p.q0 + r] = v;
     }

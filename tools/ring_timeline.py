@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--max-seq", type=int, default=2048)
     ap.add_argument("--prof", action="store_true",
                     help="the library was built with -DLLMI_RING_PROF=1 (LLMI_LIB_PATH): report wait totals")
+    ap.add_argument("--prof2", action="store_true",
+                    help="the library was built with -DLLMI_RING_PROF=2: consumer wave 0's O-phase marks")
     a = ap.parse_args()
     cfg = preset("llama2-7b", layers=a.layers, max_seq=a.max_seq)
     cfg.kv_dtype = llmi.F16
@@ -85,6 +87,14 @@ def main():
             col = col[col > 0] - t0
             marks.append([float(np.min(col)), float(np.median(col)), float(np.max(col))] if len(col) else [0, 0, 0])
         phase.append(marks)
+    if a.prof2:
+        ph = np.array(phase) / 100.0  # [layers][8 marks][min, med, max], us
+        names = ["cons_start", "merge_loads_landed", "head_merged", "wo_pieces_done", "atomics_issued",
+                 "arrived", "all_arrived", "gathered"]
+        m = ph.mean(axis=0)
+        print(json.dumps({"ctx": a.ctx, "prof2_us_min_med_max": {k: [round(float(x), 2) for x in m[i]]
+                                                                  for i, k in enumerate(names)}}))
+        return
     if a.prof:
         m = np.array(phase).mean(axis=0) / 100.0
         names = ["loader0_free_wait", "loader0_land_wait", "loader1_free_wait", "loader1_land_wait",
