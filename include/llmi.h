@@ -186,9 +186,26 @@ int llmi_kv_append(const void* k_src, const void* v_src, int dtype, int layer, c
 
 /* launchBuildCausalMasks (src/kernels/build_causal_mask.h:8-11, .cu:4-45): mask
  * [batch, max_q_len, max_k_len] = 1 where q < q_lens[b], k < k_lens[b] and
- * k_lens[b] - q_lens[b] <= k <= q + k_lens[b] - q_lens[b], else 0. */
+ * k <= q + k_lens[b] - q_lens[b], else 0. (The reference's :29 also requires
+ * k >= k_lens[b] - q_lens[b], which hides every history key from the chunk's queries;
+ * identical without history. DESIGN.md §4.) */
 int llmi_causal_mask(void* mask, int dtype, const int32_t* q_lens, const int32_t* k_lens, int batch,
                      int max_q_len, int max_k_len, llmi_stream_t stream);
+
+/* The attention core of LLaMAContextAttentionLayer::forward after the cache append
+ * (context_attention.cpp:125-161: launchRepeatKVCache -> QK^T launchLinearStridedBatchGemm
+ * -> launchScaleMaskAndSoftmax with llmi_causal_mask's mask -> PV GEMM ->
+ * launchTransposeOutRemovePadding) as ONE fused launch: q [batch, heads, max_q_len, d]
+ * (rotated, fp32), caches [layers, batch, kv_heads, max_seq, d] (dtype LLMI_F32 or
+ * LLMI_F16) of layer `layer` already holding each sequence's history and this chunk;
+ * sequence b's query s (< input_length[b]) attends to slots k <= history_length[b] + s;
+ * softmax(scale * qk) normalised by 1 / (sum + 1e-6) as the reference; out [num_tokens,
+ * heads, d] fp32 with the sequences packed in batch order (launchCalPaddingoffset's
+ * packing). head_dim 128. */
+int llmi_context_attention(const float* q, const void* k_cache, const void* v_cache, int cache_dtype, int layer,
+                           const int32_t* history_length, const int32_t* input_length, int batch, int heads,
+                           int kv_heads, int max_q_len, int max_seq, int head_dim, float scale, float* out,
+                           llmi_stream_t stream);
 
 /* launchScaleMaskAndSoftmax (src/kernels/attn_softmax_kernel.h:8-12, .cu:79-174):
  * score[b, h, q, :] = softmax(scale * qk[b, h, q, :] + (1 - mask[b, q, :]) * -10000)

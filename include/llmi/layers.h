@@ -443,6 +443,8 @@ public:
     LLaMAAttentionStaticParams& GetAttnStaticParams() { return attn_static_params; }
 
     // context_attention.cpp:26-74: buffers sized by batch_size, num_tokens, max_q_len, max_k_len
+    // (with the fused attention core -- head_size 128 -- the repeated caches, the score
+    // matrix and the padded output are never materialised, so they are not allocated)
     void allocForForward(LLaMAAttentionDynParams& p) {
         freeBuf();
         const int qkv_heads = head_num + 2 * kv_head_num, b = p.batch_size, q = p.max_q_len, k = p.max_k_len;
@@ -450,12 +452,20 @@ public:
         q_buf_w_pad = make({b, head_num, q, head_size});
         k_buf_w_pad = make({b, kv_head_num, q, head_size});
         v_buf_w_pad = make({b, kv_head_num, q, head_size});
-        k_cache_buf = make({b, head_num, k, head_size});
-        v_cache_buf = make({b, head_num, k, head_size});
-        qk_buf = make({b, head_num, q, k});
-        qkv_buf_w_pad = make({b, head_num, q, head_size});
+        if (!fused()) {
+            k_cache_buf = make({b, head_num, k, head_size});
+            v_cache_buf = make({b, head_num, k, head_size});
+            qk_buf = make({b, head_num, q, k});
+            qkv_buf_w_pad = make({b, head_num, q, head_size});
+        }
         qkv_buf_wo_pad_1 = make({p.num_tokens, head_num, head_size});
     }
+    // llmi_context_attention's shape: the whole repeat -> QK^T -> mask + softmax -> PV ->
+    // transpose chain as one launch (context_ops.hip). It applies llmi_causal_mask's mask
+    // (what LlamaContextDecoder builds, context_decoder.cpp:68-71) and ignores the
+    // "attention_mask" input; a caller with another mask calls setFusedCore(false).
+    bool fused() const { return fused_core && head_size == 128 && head_num % kv_head_num == 0; }
+    void setFusedCore(bool on) { fused_core = on; }
     void freeBuf() {
         for (auto& t : bufs) allocator->Free(t->data, false);
         bufs.clear();
@@ -487,10 +497,18 @@ public:
         // 2. RoPE (position history + s) and [num_tokens, ...] -> [bs, heads, max_q_len, head]
         launchAddFusedQKVBiasTransposeAndRoPE(q_buf_w_pad, k_buf_w_pad, v_buf_w_pad, qkv_buf_wo_pad, weights.qkv,
                                               padding_offset, history_length, input_length, static_params, stream);
-        // positions past a sequence's context are never written by the repeat: zero them,
-        // so the masked columns of QK^T / PV multiply finite values
-        LLMI_CALL(llmi_device_memset_async(k_cache_buf->data, 0, k_cache_buf->size() * sizeof(float), stream));
-        LLMI_CALL(llmi_device_memset_async(v_cache_buf->data, 0, v_cache_buf->size() * sizeof(float), stream));
+        const bool fz = fused();
+        if (!fz) {
+            // positions past a sequence's context are never written by the repeat: zero them,
+            // so the masked columns of QK^T / PV multiply finite values
+            LLMI_CALL(llmi_device_memset_async(k_cache_buf->data, 0, k_cache_buf->size() * sizeof(float), stream));
+            LLMI_CALL(llmi_device_memset_async(v_cache_buf->data, 0, v_cache_buf->size() * sizeof(float), stream));
+        }
+        void* kcache = cdt == FP32 ? (void*)outputs["all_k_cache"]->as<float>()->data
+                                   : (void*)outputs["all_k_cache"]->as<half_t>()->data;
+        void* vcache = cdt == FP32 ? (void*)outputs["all_v_cache"]->as<float>()->data
+                                   : (void*)outputs["all_v_cache"]->as<half_t>()->data;
+        const int max_seq = outputs["all_k_cache"]->shape[3];
         if (cdt == FP32) {
             TensorWrapper<float>* all_k_cache = outputs["all_k_cache"]->as<float>();
             TensorWrapper<float>* all_v_cache = outputs["all_v_cache"]->as<float>();
@@ -498,7 +516,9 @@ public:
             launchConcatKVCache(k_buf_w_pad, v_buf_w_pad, layer_id, input_length, history_length, all_k_cache,
                                 all_v_cache, stream);
             // 4. history + prompt, kv heads repeated to the query heads
-            launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, k_cache_buf, v_cache_buf, stream);
+            if (!fz)
+                launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, k_cache_buf, v_cache_buf,
+                                    stream);
         } else {
             // LLaMAContextAttentionLayer<half> (context_attention.cpp:177): the caches hold fp16.
             // The new k/v rows are rounded to fp16 as they enter the cache (what the reference's
@@ -510,6 +530,22 @@ public:
             LLMI_CALL(llmi_convert(k_buf_w_pad->data, LLMI_F32, kh->data, LLMI_F16, kh->size(), stream));
             LLMI_CALL(llmi_convert(v_buf_w_pad->data, LLMI_F32, vh->data, LLMI_F16, vh->size(), stream));
             launchConcatKVCache(kh, vh, layer_id, input_length, history_length, all_k_cache, all_v_cache, stream);
+        }
+        if (fz) {
+            // 4-5. the attention core over the layer's cache in one launch (fp16 caches are
+            // read as they are: the unfused chain widens exactly these values to fp32)
+            LLMI_CALL(llmi_context_attention(q_buf_w_pad->data, kcache, vcache, cdt == FP32 ? LLMI_F32 : LLMI_F16,
+                                             layer_id->getVal(), history_length->data, input_length->data,
+                                             params.batch_size, head_num, kv_head_num, params.max_q_len, max_seq,
+                                             head_size, scale, qkv_buf_wo_pad_1->data, stream));
+            launchLinearGemm(qkv_buf_wo_pad_1, weights.output, out.get(), c, false, true);
+            out.store();
+            freeBuf();
+            return;
+        }
+        if (cdt != FP32) {
+            TensorWrapper<half_t>* all_k_cache = outputs["all_k_cache"]->as<half_t>();
+            TensorWrapper<half_t>* all_v_cache = outputs["all_v_cache"]->as<half_t>();
             TensorWrapper<half_t>* kr = make_half(k_cache_buf->shape);
             TensorWrapper<half_t>* vr = make_half(v_cache_buf->shape);
             LLMI_CALL(llmi_device_memset_async(kr->data, 0, kr->size() * sizeof(half_t), stream));
@@ -546,6 +582,7 @@ private:
         return hbufs.back().get();
     }
     std::vector<std::unique_ptr<TensorWrapper<half_t>>> hbufs;
+    bool fused_core = true;
     int head_num, kv_head_num, head_size, hidden_units, q_head_per_kv;
     float scale;
     LLaMAAttentionStaticParams attn_static_params;
@@ -576,6 +613,8 @@ public:
           ctxAttn(head_num, kv_head_num, head_size, attn_params, stream, cublas_wrapper, allocator),
           ffn(head_num, head_size, inter_size, stream, cublas_wrapper, allocator) {}
     ~LlamaContextDecoder() { freeBuf(); }
+    // the attention core as one fused launch (default) or the reference's unfused chain
+    void setFusedAttentionCore(bool on) { ctxAttn.setFusedCore(on); }
 
     void allocForForward(LLaMAAttentionDynParams& p) {
         freeBuf();

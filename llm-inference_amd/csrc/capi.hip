@@ -178,6 +178,14 @@ int llmi_kv_append(const void* k_src, const void* v_src, int dtype, int layer, c
                             head_dim, max_seq, k_cache, v_cache, STREAM(stream));
 }
 
+int llmi_context_attention(const float* q, const void* k_cache, const void* v_cache, int cache_dtype, int layer,
+                           const int32_t* history_length, const int32_t* input_length, int batch, int heads,
+                           int kv_heads, int max_q_len, int max_seq, int head_dim, float scale, float* out,
+                           llmi_stream_t stream) {
+    return context_attention_launch(q, k_cache, v_cache, cache_dtype, layer, history_length, input_length, batch,
+                                    heads, kv_heads, max_q_len, max_seq, head_dim, scale, out, STREAM(stream));
+}
+
 int llmi_causal_mask(void* mask, int dtype, const int32_t* q_lens, const int32_t* k_lens, int batch,
                      int max_q_len, int max_k_len, llmi_stream_t stream) {
     return causal_mask_launch(mask, dtype, q_lens, k_lens, batch, max_q_len, max_k_len, STREAM(stream));

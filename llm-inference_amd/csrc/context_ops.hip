@@ -236,6 +236,159 @@ int rope_qkv_prefill_launch(const void* qkv, void* q, void* k, void* v, int dtyp
     return LLMI_OK;
 }
 
+
+// ---------------------------------------------------------------------------------
+// Fused context attention over ragged batches with history: the middle of
+// LLaMAContextAttentionLayer::forward after the cache append (context_attention.cpp:
+// 125-161: launchRepeatKVCache -> QK^T strided GEMM -> launchScaleMaskAndSoftmax with
+// the causal mask -> PV strided GEMM -> launchTransposeOutRemovePadding) as ONE launch.
+// Sequence b's query s (s < input_length[b]) attends to cache slots k <= history[b] + s
+// of kv head h / (heads / kv_heads) -- the mask llmi_causal_mask builds -- with the
+// reference softmax's normalisation 1 / (sum + 1e-6) (attn_softmax_kernel.cu); masked
+// and padded keys contribute exactly 0 there too (exp(x - 10000 - max) underflows), so
+// nothing else changes. No repeated cache, score matrix or padded output is
+// materialised: K/V rows are read from the layer's cache in 32-key LDS chunks, scores
+// and the online softmax stay in registers (fp32), and the output row lands at its
+// packed token index (sequences packed in batch order, as launchCalPaddingoffset packs
+// them). Roofline: at 512 ragged rows the layer's ~0.6 GFLOP is VALU/LDS-operand bound
+// in this fp32 form; what it removes is the unfused chain's HBM round trips
+// (b x heads x max_k x d repeated K/V, b x heads x max_q x max_k scores, padded output).
+namespace {
+constexpr int kCD = 128, kCQB = 32, kCKC = 32, kCLd = kCD + 4, kCThreads = 256;
+template <typename KT> __device__ __forceinline__ float ldc(const KT* p) { return ldf<KT>(p); }
+
+// grid (ceil(max_q / 32), heads, batch), block 256. Thread t: query row qi = t >> 3 of
+// the block; scores for keys kg + 8 c (kg = t & 7, c < 4) of a chunk; output dims
+// 4 kg + 32 r + {0..3} (r < 4).
+template <typename KT>
+__global__ __launch_bounds__(kCThreads) void ctx_attn_kernel(const float* q, const KT* k_cache, const KT* v_cache,
+                                                              const int* hist, const int* qlen, int heads,
+                                                              int kv_heads, int max_q, int max_seq, float scale,
+                                                              float* out) {
+    __shared__ float q_s[kCQB * kCLd];
+    __shared__ float k_s[kCKC * kCLd];
+    __shared__ float v_s[kCKC * kCD];
+    __shared__ float p_s[kCQB * (kCKC + 1)];
+    const int t = threadIdx.x, b = blockIdx.z, h = blockIdx.y;
+    const int ql = qlen[b], h0 = hist[b];
+    const int q_first = (gridDim.x - 1 - blockIdx.x) * kCQB;  // longest query blocks first
+    if (q_first >= ql) return;                               // uniform: a padded block
+    int tok0 = 0;
+    for (int i = 0; i < b; ++i) tok0 += qlen[i];
+    const int kvh = h / (heads / kv_heads);
+    const int qi = t >> 3, kg = t & 7;
+    const int q_row = min(q_first + qi, ql - 1);  // rows past the sequence compute, never store
+    const float* qb = q + ((size_t)b * heads + h) * max_q * kCD;
+    for (int e = t; e < kCQB * kCD; e += kCThreads) {
+        const int r = e / kCD, d = e % kCD;
+        q_s[r * kCLd + d] = qb[(size_t)min(q_first + r, ql - 1) * kCD + d];
+    }
+    const KT* kc = k_cache + ((size_t)b * kv_heads + kvh) * max_seq * kCD;
+    const KT* vc = v_cache + ((size_t)b * kv_heads + kvh) * max_seq * kCD;
+    const int my_pos = h0 + q_row;
+    const int kend = h0 + min(q_first + kCQB, ql);  // keys [0, kend)
+    float m_run = -INFINITY, l_run = 0.f;
+    float o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] = 0.f;
+    for (int k0 = 0; k0 < kend; k0 += kCKC) {
+        __syncthreads();
+        for (int e = t; e < kCKC * kCD; e += kCThreads) {
+            const int r = e / kCD, d = e % kCD;
+            const int j = min(k0 + r, kend - 1);
+            k_s[r * kCLd + d] = ldc(kc + (size_t)j * kCD + d);
+            v_s[r * kCD + d] = ldc(vc + (size_t)j * kCD + d);
+        }
+        __syncthreads();
+        float sc[4] = {0.f, 0.f, 0.f, 0.f};
+        const float* qp = q_s + qi * kCLd;
+#pragma unroll 4
+        for (int d = 0; d < kCD; d += 4) {
+            const float4 qv = *reinterpret_cast<const float4*>(qp + d);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 kv = *reinterpret_cast<const float4*>(k_s + (kg + 8 * c) * kCLd + d);
+                sc[c] = fmaf(qv.x, kv.x, sc[c]);
+                sc[c] = fmaf(qv.y, kv.y, sc[c]);
+                sc[c] = fmaf(qv.z, kv.z, sc[c]);
+                sc[c] = fmaf(qv.w, kv.w, sc[c]);
+            }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int j = k0 + kg + 8 * c;
+            sc[c] = (j > my_pos || j >= kend) ? -INFINITY : scale * sc[c];  // the reference's scale * qk
+            mx = fmaxf(mx, sc[c]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 1));
+        mx = fmaxf(mx, __shfl_xor(mx, 2));
+        mx = fmaxf(mx, __shfl_xor(mx, 4));
+        const float m_new = fmaxf(m_run, mx);  // finite: key 0 is always visible
+        const float alpha = expf(m_run - m_new);
+        float ps = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float pv = expf(sc[c] - m_new);
+            ps += pv;
+            p_s[qi * (kCKC + 1) + kg + 8 * c] = pv;
+        }
+        ps += __shfl_xor(ps, 1);
+        ps += __shfl_xor(ps, 2);
+        ps += __shfl_xor(ps, 4);
+        l_run = l_run * alpha + ps;
+        m_run = m_new;
+        __builtin_amdgcn_wave_barrier();  // a p_s row is written and read by the same 8 lanes
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[i] *= alpha;
+        const float* pr = p_s + qi * (kCKC + 1);
+#pragma unroll 4
+        for (int j = 0; j < kCKC; ++j) {
+            const float pv = pr[j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 vv = *reinterpret_cast<const float4*>(v_s + j * kCD + 4 * kg + 32 * r);
+                o[4 * r + 0] = fmaf(pv, vv.x, o[4 * r + 0]);
+                o[4 * r + 1] = fmaf(pv, vv.y, o[4 * r + 1]);
+                o[4 * r + 2] = fmaf(pv, vv.z, o[4 * r + 2]);
+                o[4 * r + 3] = fmaf(pv, vv.w, o[4 * r + 3]);
+            }
+        }
+    }
+    if (q_first + qi < ql) {
+        const float inv = 1.0f / (l_run + 1e-6f);  // attn_softmax_kernel.cu: exp(x - max) / (sum + 1e-6)
+        float* orow = out + ((size_t)(tok0 + q_first + qi) * heads + h) * kCD;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<float4*>(orow + 4 * kg + 32 * r) =
+                make_float4(o[4 * r] * inv, o[4 * r + 1] * inv, o[4 * r + 2] * inv, o[4 * r + 3] * inv);
+    }
+}
+}  // namespace
+
+int context_attention_launch(const float* q, const void* k_cache, const void* v_cache, int cache_dtype, int layer,
+                             const int* history_length, const int* input_length, int batch, int heads, int kv_heads,
+                             int max_q, int max_seq, int head_dim, float scale, float* out, hipStream_t s) {
+    LLMI_REQUIRE(q && k_cache && v_cache && history_length && input_length && out, "context_attention: null pointer");
+    LLMI_REQUIRE(head_dim == kCD, "context_attention: head_dim must be 128");
+    LLMI_REQUIRE(layer >= 0 && batch > 0 && batch <= 65535 && heads > 0 && kv_heads > 0 && heads % kv_heads == 0 &&
+                     max_q > 0 && max_seq > 0,
+                 "context_attention: bad shape");
+    LLMI_REQUIRE(fp_dtype(cache_dtype), "context_attention: cache dtype must be f32 or f16");
+    const size_t off = (size_t)layer * batch * kv_heads * max_seq * kCD;  // concat_past_kv.cu:122
+    const dim3 grid((max_q + kCQB - 1) / kCQB, heads, batch);
+    if (cache_dtype == LLMI_F32)
+        hipLaunchKernelGGL(ctx_attn_kernel<float>, grid, dim3(kCThreads), 0, s, q, (const float*)k_cache + off,
+                           (const float*)v_cache + off, history_length, input_length, heads, kv_heads, max_q, max_seq,
+                           scale, out);
+    else
+        hipLaunchKernelGGL(ctx_attn_kernel<__half>, grid, dim3(kCThreads), 0, s, q, (const __half*)k_cache + off,
+                           (const __half*)v_cache + off, history_length, input_length, heads, kv_heads, max_q,
+                           max_seq, scale, out);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
 }  // namespace llmi
 
 // ------------------------------------------------ strided batched matmul

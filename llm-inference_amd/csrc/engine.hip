@@ -49,6 +49,9 @@ namespace {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace
 
+#ifndef LLMI_F16_DOWN_KSPLIT
+#define LLMI_F16_DOWN_KSPLIT 1  // fp16 down K slices (int64 atomics: exact in any order)
+#endif
 #ifndef LLMI_I8_DOWN_KSPLIT
 #define LLMI_I8_DOWN_KSPLIT 4  // int8 down K slices: 13B down 18.2 -> 16.5 us, 8-layer loop 682 -> 665 us (A/B)
 #endif
@@ -675,7 +678,9 @@ struct Engine {
         a.epi = EPI_ATOMIC; a.yacc = res[(l + 1) % 2];
         // int8 rows are half the bytes of fp16 ones: K slices keep the loads per row in
         // flight and the x image per workgroup small (exact: int64 atomics)
-        a.ksplit = (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT : 1;
+        a.ksplit = (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT
+                   : (wdt == LLMI_F16 && il % (8 * LLMI_F16_DOWN_KSPLIT) == 0) ? LLMI_F16_DOWN_KSPLIT
+                                                                               : 1;
         return a;
     }
 

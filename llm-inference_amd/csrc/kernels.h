@@ -335,6 +335,10 @@ int causal_mask_launch(void* mask, int dtype, const int* q_lens, const int* k_le
                        hipStream_t s);
 int masked_softmax_launch(const void* qk, const void* mask, void* score, int dtype, int batch, int heads, int q_len,
                           int k_len, float scale, hipStream_t s);
+// fused ragged-batch context attention over the layer's cache (context_ops.hip)
+int context_attention_launch(const float* q, const void* k_cache, const void* v_cache, int cache_dtype, int layer,
+                             const int* history_length, const int* input_length, int batch, int heads, int kv_heads,
+                             int max_q, int max_seq, int head_dim, float scale, float* out, hipStream_t s);
 int kv_append_launch(const void* k_src, const void* v_src, int dtype, int layer, const int* cur_q, const int* hist,
                      int batch, int kv_heads, int max_q, int d, int max_seq, void* k_cache, void* v_cache,
                      hipStream_t s);

@@ -4,9 +4,11 @@
 // after them (rope at history + t, KV concat at slot history + t, causal mask over
 // history + chunk). Inputs from <dir>/*.bin, outputs to <dir>/out_*.bin for the pytest
 // driver (tests/test_gpu_ctx_history.py):
-//   test_ctx_history <dir> <heads> <kv_heads> <head> <inter> <layers> <vocab> <max_seq> <seed> <bs> [f16]
+//   test_ctx_history <dir> <heads> <kv_heads> <head> <inter> <layers> <vocab> <max_seq> <seed> <bs> [f16|f32] [unfused]
 // With "f16" the caches are TensorWrapper<half> (LLaMAContextAttentionLayer<half>,
 // context_attention.cpp:177): uploaded rounded to fp16, written back widened to fp32.
+// "unfused": the reference's attention chain (repeat, QK^T, mask + softmax, PV,
+// transpose) instead of the fused llmi_context_attention core.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -52,6 +54,7 @@ int main(int argc, char** argv) {
         const uint64_t seed = std::strtoull(argv[9], nullptr, 10);
         const int bs = std::atoi(argv[10]);
         const bool f16 = argc > 11 && std::string(argv[11]) == "f16";
+        const bool unfused = argc > 12 && std::string(argv[12]) == "unfused";
         const int H = heads * hd;
         const std::vector<int> hist = load<int>(dir + "/hist.bin", bs), lens = load<int>(dir + "/lens.bin", bs);
         int tokens = 0, maxq = 0, maxk = 0;
@@ -106,6 +109,7 @@ int main(int argc, char** argv) {
         TensorWrapper<int> layer_t(CPU, INT32, {1}, &layer0);
         launchInputEmbedding(&id_t, &in, &E);
         LlamaContextDecoder<half_t> dec(heads, kv, hd, I, L, sp, 1e-5f, nullptr, nullptr, &g_alloc);
+        dec.setFusedAttentionCore(!unfused);
         LLaMAAttentionDynParams p;
         p.batch_size = bs;
         p.num_tokens = tokens;

@@ -3,6 +3,7 @@
 // the MFMA GEMM (llmi_linear, fp32-faithful split), QK^T / PV on the MFMA batched matmul,
 // mask/softmax/transpose as their own launches. Random-init weights (llmi-prng), 32 layers.
 //   ctx_decoder_bench <layers> <reps> <len0> [len1 ...]      (history 0, max_seq = max len)
+// LLMI_CTX_UNFUSED=1: the reference's unfused attention chain instead of the fused core.
 // (per-forward scratch through HipCachingAllocator, as the reference's CudaAllocator).
 // Prints one JSON line: ms per forward over the batch, rows/s.
 #include <algorithm>
@@ -62,6 +63,9 @@ int main(int argc, char** argv) {
         int layer0 = 0;
         TensorWrapper<int> layer_t(CPU, INT32, {1}, &layer0);
         LlamaContextDecoder<half_t> dec(heads, kv, hd, I, L, sp, 1e-5f, nullptr, nullptr, &g_alloc);
+        const char* uf = std::getenv("LLMI_CTX_UNFUSED");
+        const bool unfused = uf && std::string(uf) == "1";
+        dec.setFusedAttentionCore(!unfused);
         LLaMAAttentionDynParams p;
         p.batch_size = bs;
         p.num_tokens = tokens;
@@ -84,8 +88,8 @@ int main(int argc, char** argv) {
         std::string ls;
         for (int l : lens) ls += (ls.empty() ? "" : ",") + std::to_string(l);
         std::printf("{\"api\": \"LlamaContextDecoder<half>::forward\", \"layers\": %d, \"lens\": [%s], \"rows\": %d, "
-                    "\"ms_best\": %.3f, \"ms_mean\": %.3f, \"rows_per_s\": %.1f}\n",
-                    L, ls.c_str(), tokens, best, sum / reps, tokens / (best * 1e-3));
+                    "\"ms_best\": %.3f, \"ms_mean\": %.3f, \"rows_per_s\": %.1f, \"attention_core\": \"%s\"}\n",
+                    L, ls.c_str(), tokens, best, sum / reps, tokens / (best * 1e-3), unfused ? "unfused" : "fused");
         for (auto* w : lw) delete w;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
