@@ -88,6 +88,16 @@ int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llm
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m,
                 int n, int k, llmi_stream_t stream);
 
+/* LLaMAFFNLayer::forward (ffn.cpp:52-93) for context rows as one call: y [m, hidden] =
+ * W_down (silu(W_gate x) * (W_up x)), x [m, hidden] fp32, w_gate_up [2 inter, hidden] (gate
+ * rows then up rows, the reference's fused gate_up_proj) and w_down [hidden, inter] fp16.
+ * On the matrix cores with fp32-faithful split activations (llmi_linear's arithmetic); the
+ * SiLU*up product goes from the gate_up epilogue straight into the down GEMM's input, never
+ * to memory in fp32. LLMI_EUNSUPPORTED (nothing launched) for other dtypes / shapes: the
+ * caller then runs llmi_linear + llmi_silu_mul + llmi_linear. */
+int llmi_ffn(const float* x, const void* w_gate_up, const void* w_down, int w_dtype, float* y, int m, int hidden,
+             int inter, llmi_stream_t stream);
+
 /* One decode row through the HBM-streaming GEMV with its fused prologue/epilogue -- what
  * LlamaSelfDecoder::forward strings together for a token (self_decoder.cpp:59-81 fused):
  *   gamma != NULL: x is RMS-normalised and scaled by gamma (dtype gamma_dtype) first;
@@ -206,6 +216,18 @@ int llmi_context_attention(const float* q, const void* k_cache, const void* v_ca
                            const int32_t* history_length, const int32_t* input_length, int batch, int heads,
                            int kv_heads, int max_q_len, int max_seq, int head_dim, float scale, float* out,
                            llmi_stream_t stream);
+
+/* The same core with the two launchers in front of it fused in (launchAddFusedQKVBiasTransposeAndRoPE
+ * + launchConcatKVCache, context_attention.cpp:108-124): qkv [num_tokens, (heads + 2 kv_heads) d]
+ * fp32 rows (padding_offset as llmi_padding_offset makes it) are rotated at position
+ * history_length[b] + s (llmi_rope_qkv_prefill's arithmetic), q goes to q_scratch [batch,
+ * heads, max_q_len, d] and k / v straight into the cache slots llmi_kv_append would write
+ * (rounded to the cache dtype), then llmi_context_attention runs. */
+int llmi_context_attention_qkv(const float* qkv, const int32_t* padding_offset, const int32_t* history_length,
+                               const int32_t* input_length, int num_tokens, int batch, int max_q_len, int heads,
+                               int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
+                               int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
+                               llmi_stream_t stream);
 
 /* launchScaleMaskAndSoftmax (src/kernels/attn_softmax_kernel.h:8-12, .cu:79-174):
  * score[b, h, q, :] = softmax(scale * qk[b, h, q, :] + (1 - mask[b, q, :]) * -10000)

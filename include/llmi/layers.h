@@ -268,6 +268,20 @@ public:
         llmi_detail::ActF32 out(outputs["ffn_output"], allocator, stream, false, "LLaMAFFNLayer");
         cublasWrapper cw{stream};
         cublasWrapper* c = cublas_wrapper ? cublas_wrapper : &cw;
+        const int rows = params.is_ctx ? params.num_tokens : params.batch_size;
+        // context rows with fp16 weights: gate_up + SiLU*up + down in one fused call
+        // (llmi_ffn; same products as the three launches below, the SiLU*up rows handed to
+        // the down GEMM as its fp16 input planes instead of an fp32 buffer)
+        const int rc = (params.is_ctx && rows >= 16 && getTensorType<T>() == FP16 &&
+                        weights.gateAndup.type == WeightType::FP16_W && weights.down.type == WeightType::FP16_W)
+                           ? llmi_ffn(in.get()->data, weights.gateAndup.data, weights.down.data, LLMI_F16,
+                                      out.get()->data, rows, hidden, inter_size, stream)
+                           : LLMI_EUNSUPPORTED;
+        if (rc == LLMI_OK) {
+            out.store();
+            return;
+        }
+        if (rc != LLMI_EUNSUPPORTED) LLMI_CALL(rc);
         launchLinearGemm(in.get(), weights.gateAndup, SwiGLU_input.get(), c, false, true);
         launchAct(SwiGLU_input.get(), down_proj_input.get(), stream);
         launchLinearGemm(down_proj_input.get(), weights.down, out.get(), c, false, true);
@@ -450,9 +464,9 @@ public:
         const int qkv_heads = head_num + 2 * kv_head_num, b = p.batch_size, q = p.max_q_len, k = p.max_k_len;
         qkv_buf_wo_pad = make({p.num_tokens, qkv_heads, head_size});
         q_buf_w_pad = make({b, head_num, q, head_size});
-        k_buf_w_pad = make({b, kv_head_num, q, head_size});
-        v_buf_w_pad = make({b, kv_head_num, q, head_size});
         if (!fused()) {
+            k_buf_w_pad = make({b, kv_head_num, q, head_size});
+            v_buf_w_pad = make({b, kv_head_num, q, head_size});
             k_cache_buf = make({b, head_num, k, head_size});
             v_cache_buf = make({b, head_num, k, head_size});
             qk_buf = make({b, head_num, q, k});
@@ -494,21 +508,32 @@ public:
         llmi_detail::ActF32 out(outputs["attention_output"], allocator, stream, false, "LLaMAContextAttentionLayer");
         // 1. qkv linear
         launchLinearGemm(in.get(), weights.qkv, qkv_buf_wo_pad, c, false, true);
-        // 2. RoPE (position history + s) and [num_tokens, ...] -> [bs, heads, max_q_len, head]
-        launchAddFusedQKVBiasTransposeAndRoPE(q_buf_w_pad, k_buf_w_pad, v_buf_w_pad, qkv_buf_wo_pad, weights.qkv,
-                                              padding_offset, history_length, input_length, static_params, stream);
-        const bool fz = fused();
-        if (!fz) {
-            // positions past a sequence's context are never written by the repeat: zero them,
-            // so the masked columns of QK^T / PV multiply finite values
-            LLMI_CALL(llmi_device_memset_async(k_cache_buf->data, 0, k_cache_buf->size() * sizeof(float), stream));
-            LLMI_CALL(llmi_device_memset_async(v_cache_buf->data, 0, v_cache_buf->size() * sizeof(float), stream));
-        }
+        const int max_seq = outputs["all_k_cache"]->shape[3];
         void* kcache = cdt == FP32 ? (void*)outputs["all_k_cache"]->as<float>()->data
                                    : (void*)outputs["all_k_cache"]->as<half_t>()->data;
         void* vcache = cdt == FP32 ? (void*)outputs["all_v_cache"]->as<float>()->data
                                    : (void*)outputs["all_v_cache"]->as<half_t>()->data;
-        const int max_seq = outputs["all_k_cache"]->shape[3];
+        if (fused()) {
+            // 2-5 fused: RoPE with the k / v rows stored straight into the cache after the
+            // history, then the attention core over the cache (one launch each; fp16 caches
+            // are read as they are: the unfused chain widens exactly these values to fp32)
+            LLMI_CALL(llmi_context_attention_qkv(
+                qkv_buf_wo_pad->data, padding_offset->data, history_length->data, input_length->data, params.num_tokens,
+                params.batch_size, params.max_q_len, head_num, kv_head_num, head_size,
+                static_params.rotary_embedding_base, kcache, vcache, cdt == FP32 ? LLMI_F32 : LLMI_F16,
+                layer_id->getVal(), max_seq, scale, q_buf_w_pad->data, qkv_buf_wo_pad_1->data, stream));
+            launchLinearGemm(qkv_buf_wo_pad_1, weights.output, out.get(), c, false, true);
+            out.store();
+            freeBuf();
+            return;
+        }
+        // 2. RoPE (position history + s) and [num_tokens, ...] -> [bs, heads, max_q_len, head]
+        launchAddFusedQKVBiasTransposeAndRoPE(q_buf_w_pad, k_buf_w_pad, v_buf_w_pad, qkv_buf_wo_pad, weights.qkv,
+                                              padding_offset, history_length, input_length, static_params, stream);
+        // positions past a sequence's context are never written by the repeat: zero them,
+        // so the masked columns of QK^T / PV multiply finite values
+        LLMI_CALL(llmi_device_memset_async(k_cache_buf->data, 0, k_cache_buf->size() * sizeof(float), stream));
+        LLMI_CALL(llmi_device_memset_async(v_cache_buf->data, 0, v_cache_buf->size() * sizeof(float), stream));
         if (cdt == FP32) {
             TensorWrapper<float>* all_k_cache = outputs["all_k_cache"]->as<float>();
             TensorWrapper<float>* all_v_cache = outputs["all_v_cache"]->as<float>();
@@ -516,9 +541,7 @@ public:
             launchConcatKVCache(k_buf_w_pad, v_buf_w_pad, layer_id, input_length, history_length, all_k_cache,
                                 all_v_cache, stream);
             // 4. history + prompt, kv heads repeated to the query heads
-            if (!fz)
-                launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, k_cache_buf, v_cache_buf,
-                                    stream);
+            launchRepeatKVCache(all_k_cache, all_v_cache, context_length, layer_id, k_cache_buf, v_cache_buf, stream);
         } else {
             // LLaMAContextAttentionLayer<half> (context_attention.cpp:177): the caches hold fp16.
             // The new k/v rows are rounded to fp16 as they enter the cache (what the reference's
@@ -530,22 +553,6 @@ public:
             LLMI_CALL(llmi_convert(k_buf_w_pad->data, LLMI_F32, kh->data, LLMI_F16, kh->size(), stream));
             LLMI_CALL(llmi_convert(v_buf_w_pad->data, LLMI_F32, vh->data, LLMI_F16, vh->size(), stream));
             launchConcatKVCache(kh, vh, layer_id, input_length, history_length, all_k_cache, all_v_cache, stream);
-        }
-        if (fz) {
-            // 4-5. the attention core over the layer's cache in one launch (fp16 caches are
-            // read as they are: the unfused chain widens exactly these values to fp32)
-            LLMI_CALL(llmi_context_attention(q_buf_w_pad->data, kcache, vcache, cdt == FP32 ? LLMI_F32 : LLMI_F16,
-                                             layer_id->getVal(), history_length->data, input_length->data,
-                                             params.batch_size, head_num, kv_head_num, params.max_q_len, max_seq,
-                                             head_size, scale, qkv_buf_wo_pad_1->data, stream));
-            launchLinearGemm(qkv_buf_wo_pad_1, weights.output, out.get(), c, false, true);
-            out.store();
-            freeBuf();
-            return;
-        }
-        if (cdt != FP32) {
-            TensorWrapper<half_t>* all_k_cache = outputs["all_k_cache"]->as<half_t>();
-            TensorWrapper<half_t>* all_v_cache = outputs["all_v_cache"]->as<half_t>();
             TensorWrapper<half_t>* kr = make_half(k_cache_buf->shape);
             TensorWrapper<half_t>* vr = make_half(v_cache_buf->shape);
             LLMI_CALL(llmi_device_memset_async(kr->data, 0, kr->size() * sizeof(half_t), stream));

@@ -51,6 +51,19 @@ int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llm
     return silu_mul_launch(gate_up, out, n_tokens, inter, STREAM(stream));
 }
 
+int llmi_ffn(const float* x, const void* w_gate_up, const void* w_down, int w_dtype, float* y, int m, int hidden,
+             int inter, llmi_stream_t stream) {
+    LLMI_REQUIRE(x && w_gate_up && w_down && y && m >= 1 && hidden >= 1 && inter >= 1, "ffn: bad arguments");
+    if (w_dtype != LLMI_F16 || !ffn_mfma_supported(m, hidden, inter) || (reinterpret_cast<uintptr_t>(x) & 15) ||
+        (reinterpret_cast<uintptr_t>(y) & 15) || (reinterpret_cast<uintptr_t>(w_gate_up) & 15) ||
+        (reinterpret_cast<uintptr_t>(w_down) & 15)) {
+        set_last_error("[llmi][ERROR] ffn: the fused context FFN needs fp16 weights, M >= 16, 16-B aligned buffers "
+                       "and GEMM-tileable hidden / inter (use llmi_linear + llmi_silu_mul)");
+        return LLMI_EUNSUPPORTED;
+    }
+    return ffn_mfma_launch(x, w_gate_up, w_down, y, m, hidden, inter, STREAM(stream));
+}
+
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
                 llmi_stream_t stream) {
     LLMI_REQUIRE(m >= 1 && n >= 1 && k >= 1, "linear: m, n, k must be >= 1");
@@ -184,6 +197,16 @@ int llmi_context_attention(const float* q, const void* k_cache, const void* v_ca
                            llmi_stream_t stream) {
     return context_attention_launch(q, k_cache, v_cache, cache_dtype, layer, history_length, input_length, batch,
                                     heads, kv_heads, max_q_len, max_seq, head_dim, scale, out, STREAM(stream));
+}
+
+int llmi_context_attention_qkv(const float* qkv, const int32_t* padding_offset, const int32_t* history_length,
+                               const int32_t* input_length, int num_tokens, int batch, int max_q_len, int heads,
+                               int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
+                               int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
+                               llmi_stream_t stream) {
+    return context_attention_qkv_launch(qkv, padding_offset, history_length, input_length, num_tokens, batch,
+                                        max_q_len, heads, kv_heads, head_dim, rope_base, k_cache, v_cache, cache_dtype,
+                                        layer, max_seq, scale, q_scratch, out, STREAM(stream));
 }
 
 int llmi_causal_mask(void* mask, int dtype, const int32_t* q_lens, const int32_t* k_lens, int batch,

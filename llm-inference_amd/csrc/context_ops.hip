@@ -114,6 +114,15 @@ __device__ __forceinline__ void rope_angle(int pos, int i, int d, float base, fl
     *s = (float)sd;
 }
 
+// the rotated pair (x0 c - x1 s, x1 c + x0 s) with every product and sum rounded on its own
+// (no fma contraction), so the launcher and the fused-to-cache form below give the same bits
+__device__ __forceinline__ float rot_lo(float x0, float x1, float c, float s) {
+    return __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
+}
+__device__ __forceinline__ float rot_hi(float x0, float x1, float c, float s) {
+    return __fadd_rn(__fmul_rn(x1, c), __fmul_rn(x0, s));
+}
+
 // add_fusedQKV_bias_transpose_kernel (qkv_bias_and_RoPE.cu:49-144), Llama (no bias):
 // grid (num_tokens, heads), block d. Threads < d/2 rotate the pair (i, i + d/2) of q
 // (and of k for head < kv_heads); every thread of a head < kv_heads copies v.
@@ -130,16 +139,51 @@ __global__ void rope_qkv_prefill_kernel(const T* qkv, T* q_buf, T* k_buf, T* v_b
         rope_angle(hist[b] + s, t, d, base, &c, &sn);
         const T* qh = row + (size_t)h * d;
         const float q0 = ldf(qh + t), q1 = ldf(qh + t + d / 2);
-        stf(q_buf + qo + t, q0 * c - q1 * sn);
-        stf(q_buf + qo + t + d / 2, q1 * c + q0 * sn);
+        stf(q_buf + qo + t, rot_lo(q0, q1, c, sn));
+        stf(q_buf + qo + t + d / 2, rot_hi(q0, q1, c, sn));
         if (h < kv_heads) {
             const T* kh = row + (size_t)(heads + h) * d;
             const float k0 = ldf(kh + t), k1 = ldf(kh + t + d / 2);
-            stf(k_buf + ko + t, k0 * c - k1 * sn);
-            stf(k_buf + ko + t + d / 2, k1 * c + k0 * sn);
+            stf(k_buf + ko + t, rot_lo(k0, k1, c, sn));
+            stf(k_buf + ko + t + d / 2, rot_hi(k0, k1, c, sn));
         }
     }
     if (h < kv_heads && t < d) v_buf[ko + t] = row[(size_t)(heads + kv_heads + h) * d + t];
+}
+
+// The same rotation with the new k / v rows stored straight into the layer's cache at
+// slot history[b] + s (launchConcatKVCache's placement, concat_past_kv.cu:122), rounded
+// to KT on the store -- what the separate append stores -- so the padded k / v buffers
+// are never written. fp32 activations.
+template <typename KT>
+__global__ void rope_qkv_cache_kernel(const float* qkv, float* q_buf, KT* k_cache, KT* v_cache, const int* po,
+                                      const int* hist, int seq_len, int heads, int kv_heads, int d, float base,
+                                      int max_seq) {
+    const int tok = blockIdx.x, h = blockIdx.y, t = threadIdx.x;
+    const int p = tok + po[tok], b = p / seq_len, s = p % seq_len;
+    const float* row = qkv + (size_t)tok * (heads + 2 * kv_heads) * d;
+    const size_t qo = (((size_t)b * heads + h) * seq_len + s) * d;
+    const size_t co = (((size_t)b * kv_heads + h) * max_seq + hist[b] + s) * d;
+    if (t < d / 2) {
+        float c, sn;
+        rope_angle(hist[b] + s, t, d, base, &c, &sn);
+        const float* qh = row + (size_t)h * d;
+        const float q0 = qh[t], q1 = qh[t + d / 2];
+        q_buf[qo + t] = rot_lo(q0, q1, c, sn);
+        q_buf[qo + t + d / 2] = rot_hi(q0, q1, c, sn);
+        if (h < kv_heads) {
+            const float* kh = row + (size_t)(heads + h) * d;
+            const float k0 = kh[t], k1 = kh[t + d / 2];
+            float r0 = rot_lo(k0, k1, c, sn), r1 = rot_hi(k0, k1, c, sn);
+            // keep the fp32 result: with a half cache the compiler would otherwise fold the
+            // last product and the conversion into one v_fma_mix (a single rounding to fp16),
+            // while the launcher + append round twice (fp32, then fp16)
+            asm volatile("" : "+v"(r0), "+v"(r1));
+            stf(k_cache + co + t, r0);
+            stf(k_cache + co + t + d / 2, r1);
+        }
+    }
+    if (h < kv_heads && t < d) stf(v_cache + co + t, row[(size_t)(heads + kv_heads + h) * d + t]);
 }
 
 bool fp_dtype(int dt) { return dt == LLMI_F32 || dt == LLMI_F16; }
@@ -387,6 +431,31 @@ int context_attention_launch(const float* q, const void* k_cache, const void* v_
                            max_seq, scale, out);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
+}
+
+int context_attention_qkv_launch(const float* qkv, const int* padding_offset, const int* history_length,
+                                 const int* input_length, int num_tokens, int batch, int max_q, int heads,
+                                 int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
+                                 int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
+                                 hipStream_t s) {
+    LLMI_REQUIRE(qkv && padding_offset && k_cache && v_cache && q_scratch, "context_attention_qkv: null pointer");
+    LLMI_REQUIRE(num_tokens > 0 && num_tokens <= batch * max_q && head_dim == kCD && kv_heads > 0 &&
+                     heads % kv_heads == 0 && heads <= 65535,
+                 "context_attention_qkv: bad shape");
+    LLMI_REQUIRE(fp_dtype(cache_dtype), "context_attention_qkv: cache dtype must be f32 or f16");
+    const size_t off = (size_t)layer * batch * kv_heads * max_seq * kCD;
+    const dim3 grid(num_tokens, heads);
+    if (cache_dtype == LLMI_F32)
+        hipLaunchKernelGGL(rope_qkv_cache_kernel<float>, grid, dim3(kCD), 0, s, qkv, q_scratch,
+                           (float*)k_cache + off, (float*)v_cache + off, padding_offset, history_length, max_q,
+                           heads, kv_heads, kCD, rope_base, max_seq);
+    else
+        hipLaunchKernelGGL(rope_qkv_cache_kernel<__half>, grid, dim3(kCD), 0, s, qkv, q_scratch,
+                           (__half*)k_cache + off, (__half*)v_cache + off, padding_offset, history_length, max_q,
+                           heads, kv_heads, kCD, rope_base, max_seq);
+    LLMI_HIP(hipGetLastError());
+    return context_attention_launch(q_scratch, k_cache, v_cache, cache_dtype, layer, history_length, input_length,
+                                    batch, heads, kv_heads, max_q, max_seq, head_dim, scale, out, s);
 }
 
 }  // namespace llmi

@@ -517,4 +517,66 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
     return LLMI_OK;
 }
 
+// LLaMAFFNLayer::forward (ffn.cpp:52-93) for the context phase in three launches on the
+// matrix cores: x -> fp16 hi/lo planes; gate_up whose epilogue writes silu(g) * u straight
+// as the down GEMM's input planes (gemm3 / gemm2 EPI_SILU_MUL, the engine prefill's
+// form: no fp32 [m, 2 I] product and no separate SiLU pass); down with the K slices of
+// llmi_linear summed in slice order. fp16 weights; fp32 x and y.
+bool ffn_mfma_supported(int m, int hidden, int inter) {
+    const bool g3 = m >= 256 && gemm3_supported(2 * inter, hidden, EPI_SILU_MUL, 1);
+    return m >= 16 && hidden % 64 == 0 && inter % 64 == 0 &&
+           (g3 || gemm2_supported(2 * inter, hidden, EPI_SILU_MUL)) && linear_mfma_supported(m, hidden, inter);
+}
+
+int ffn_mfma_launch(const float* x, const void* w_gu, const void* w_down, float* y, int m, int hidden, int inter,
+                    hipStream_t s) {
+    LLMI_REQUIRE(x && w_gu && w_down && y && ffn_mfma_supported(m, hidden, inter),
+                 "ffn_mfma: unsupported shape (M >= 16, hidden and inter multiples of 64 the GEMMs tile)");
+    LLMI_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
+                 "ffn_mfma: x and y must be 16-B aligned");
+    const bool g3gu = m >= 256 && gemm3_supported(2 * inter, hidden, EPI_SILU_MUL, 1);
+    const bool g3d = m >= 256 && gemm3_supported(hidden, inter, EPI_STORE, 1);
+    const int tiles = g3d ? ((m + 255) / 256) * (hidden / 256) : ((m + 127) / 128) * (hidden / kBN);
+    int ks = 1;
+    while (tiles * ks < 160 && ks < 8) {
+        const int nk = ks * 2;
+        if (g3d ? !gemm3_supported(hidden, inter, EPI_SLAB, nk) : inter % (nk * kBK) != 0) break;
+        ks = nk;
+    }
+    const size_t xplane = ((size_t)m * hidden * 2 + 255) / 256 * 256;
+    const size_t aplane = ((size_t)m * inter * 2 + 255) / 256 * 256;
+    const size_t slab = ks > 1 ? (size_t)ks * m * hidden * 4 : 0;
+    char* ws = nullptr;
+    LLMI_TRY(linear_workspace(s, 2 * xplane + 2 * aplane + slab, &ws));
+    _Float16* xh = reinterpret_cast<_Float16*>(ws);
+    _Float16* xl = reinterpret_cast<_Float16*>(ws + xplane);
+    _Float16* ah = reinterpret_cast<_Float16*>(ws + 2 * xplane);
+    _Float16* al = reinterpret_cast<_Float16*>(ws + 2 * xplane + aplane);
+    const size_t n4x = (size_t)m * hidden / 4;
+    hipLaunchKernelGGL(planes_kernel, dim3(grid_of(n4x)), dim3(kThreads), 0, s, reinterpret_cast<const float4*>(x), xh,
+                       xl, n4x);
+    LLMI_HIP(hipGetLastError());
+    Gemm2Args g;
+    g.a[0] = xh; g.a[1] = xl; g.planes = 2; g.lda = hidden;
+    g.w = w_gu; g.m = m; g.n = 2 * inter; g.k = hidden;
+    g.epi = EPI_SILU_MUL; g.pair_off = inter; g.y = nullptr; g.y_hi = ah; g.y_lo = al; g.ldy = inter;
+    LLMI_TRY(g3gu ? gemm3_launch(g, s) : gemm2_launch(g, s));
+    Gemm2Args d;
+    d.a[0] = ah; d.a[1] = al; d.planes = 2; d.lda = inter;
+    d.w = w_down; d.m = m; d.n = hidden; d.k = inter; d.ldy = hidden;
+    if (ks > 1) {
+        d.epi = EPI_SLAB; d.ksplit = ks; d.slab = reinterpret_cast<float*>(ws + 2 * xplane + 2 * aplane); d.y = y;
+    } else {
+        d.epi = EPI_STORE; d.y = y;
+    }
+    LLMI_TRY(g3d ? gemm3_launch(d, s) : gemm2_launch(d, s));
+    if (ks > 1) {
+        const size_t n4y = (size_t)m * hidden / 4;
+        hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_of(n4y)), dim3(kThreads), 0, s,
+                           reinterpret_cast<const float4*>(d.slab), reinterpret_cast<float4*>(y), ks, n4y);
+        LLMI_HIP(hipGetLastError());
+    }
+    return LLMI_OK;
+}
+
 }  // namespace llmi

@@ -138,6 +138,10 @@ size_t gemm3_bal_slab_bytes(int m, int n);
 // rows of 2 cols bytes with the first cols used (the fp16 row stride, gemm3.hip); synchronises s
 int w8_prepare(const void* w16, int rows, int cols, void* w8, int* exp_out, hipStream_t s);
 bool gemm2_supported(int n, int k, int epi);
+// the context FFN (gate_up + SiLU*up + down) on the matrix cores, fp16 weights (gemm2.hip)
+bool ffn_mfma_supported(int m, int hidden, int inter);
+int ffn_mfma_launch(const float* x, const void* w_gu, const void* w_down, float* y, int m, int hidden, int inter,
+                    hipStream_t s);
 int gemm2_launch(Gemm2Args a, hipStream_t s);
 // the same GEMM on 256 x 256 tiles with a ping-pong 8-wave schedule (gemm3.hip)
 bool gemm3_supported(int n, int k, int epi, int ksplit);
@@ -339,6 +343,12 @@ int masked_softmax_launch(const void* qk, const void* mask, void* score, int dty
 int context_attention_launch(const float* q, const void* k_cache, const void* v_cache, int cache_dtype, int layer,
                              const int* history_length, const int* input_length, int batch, int heads, int kv_heads,
                              int max_q, int max_seq, int head_dim, float scale, float* out, hipStream_t s);
+// + RoPE and the cache append in front (the layer's whole middle from the q/k/v rows)
+int context_attention_qkv_launch(const float* qkv, const int* padding_offset, const int* history_length,
+                                 const int* input_length, int num_tokens, int batch, int max_q, int heads,
+                                 int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
+                                 int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
+                                 hipStream_t s);
 int kv_append_launch(const void* k_src, const void* v_src, int dtype, int layer, const int* cur_q, const int* hist,
                      int batch, int kv_heads, int max_q, int d, int max_seq, void* k_cache, void* v_cache,
                      hipStream_t s);

@@ -57,6 +57,10 @@ _SIGS = {
     "llmi_kv_append": (_I, [_P, _P, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "llmi_causal_mask": (_I, [_P, _I, _P, _P, _I, _I, _I, _P]),
     "llmi_masked_softmax": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _P]),
+    "llmi_context_attention": (_I, [_P, _P, _P, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P]),
+    "llmi_context_attention_qkv": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _I, _I, _I, _F, _P,
+                                        _P, _P]),
+    "llmi_ffn": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _P]),
     "llmi_batched_matmul": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_transpose_remove_pad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_synth_fill": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I, _P]),
