@@ -51,6 +51,10 @@
 
 #include "kernels.h"
 
+#ifndef LLMI_G3_PIN8
+#define LLMI_G3_PIN8 1  // 0: let the compiler place the fp8 lo MFMAs (A/B builds only)
+#endif
+
 namespace llmi {
 
 namespace {
@@ -207,6 +211,16 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
             for (int j = 0; j < 2; ++j)
                 c[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(af[i][0], af[i][1]), cat8(bf[j][0], bf[j][1]),
                                                                           c[i][j], 0, 0, 0, sc, 1, sc);
+        // pin the 8 MFMAs inside this phase: they are register-only, and without a use here
+        // the compiler sank 3 of every 4 quadrants' fp8 MFMAs past the phase barriers (the
+        // .s had 18 of 24 set-priority windows empty and 16-MFMA bunches elsewhere), which
+        // broke the two groups' read / MFMA alternation of the lo pass
+#if LLMI_G3_PIN8
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(c[i][j]));
+#endif
         __builtin_amdgcn_s_setprio(0);
     };
     auto sync_reads = [&](int n) {  // DMA counted, then the barrier; LDS reads retire behind it
