@@ -7,6 +7,8 @@ through the C ABI on torch's current stream and raises on a non-zero status.
 """
 from __future__ import annotations
 
+import math
+
 import torch
 
 from . import _lib
@@ -235,6 +237,38 @@ def launchTransposeOutRemovePadding(src, padding_offset, num_tokens: int):
     call("llmi_transpose_remove_pad", src.data_ptr(), po.data_ptr(), out.data_ptr(), _dt(src), num_tokens, b, s, h,
          d, _stream())
     return out
+
+
+def context_attention_qkv(qkv, padding_offset, history_length, input_length, batch: int, max_q_len: int,
+                          heads: int, kv_heads: int, k_cache, v_cache, layer: int = 0, base: float = 10000.0,
+                          scale: float = None):
+    """LLaMAContextAttentionLayer's middle fused (llmi_context_attention_qkv): qkv rows
+    [num_tokens, (heads + 2 kv) * 128] fp32 -> RoPE, k / v into the caches [layers, batch, kv,
+    max_seq, 128] (fp32 or fp16) after each sequence's history, ragged causal attention ->
+    [num_tokens, heads * 128] fp32."""
+    _dev(qkv, padding_offset, history_length, input_length, k_cache, v_cache)
+    n, d = qkv.shape[0], 128
+    po, hist, ql = _i32(padding_offset), _i32(history_length), _i32(input_length)
+    qs = torch.empty(batch, heads, max_q_len, d, device=qkv.device, dtype=torch.float32)
+    out = torch.empty(n, heads * d, device=qkv.device, dtype=torch.float32)
+    sc = 1.0 / math.sqrt(d) if scale is None else scale
+    call("llmi_context_attention_qkv", qkv.contiguous().data_ptr(), po.data_ptr(), hist.data_ptr(), ql.data_ptr(), n,
+         batch, max_q_len, heads, kv_heads, d, float(base), k_cache.data_ptr(), v_cache.data_ptr(), _dt(k_cache),
+         int(layer), k_cache.shape[3], float(sc), qs.data_ptr(), out.data_ptr(), _stream())
+    return out
+
+
+def ffn(x, w_gate_up, w_down):
+    """LLaMAFFNLayer for context rows in one call (llmi_ffn): x [m, hidden] fp32, w_gate_up
+    [2 inter, hidden] and w_down [hidden, inter] fp16 -> [m, hidden] fp32. Raises
+    LlmiError (unsupported) where the fused form does not apply."""
+    _dev(x, w_gate_up, w_down)
+    m, hidden = x.shape
+    inter = w_down.shape[1]
+    y = torch.empty(m, hidden, device=x.device, dtype=torch.float32)
+    call("llmi_ffn", x.contiguous().data_ptr(), w_gate_up.data_ptr(), w_down.data_ptr(), _dt(w_gate_up), y.data_ptr(),
+         m, hidden, inter, _stream())
+    return y
 
 
 def launchLinearStridedBatchGemm(input1, input2, trans_a: bool = False, trans_b: bool = False):

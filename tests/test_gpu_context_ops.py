@@ -254,3 +254,68 @@ def test_padding_offset_reference_example(ops):
     po, cum = ops.launchCalPaddingoffset(T(np.array([5, 4, 7, 6], np.int32)), 8)
     np.testing.assert_array_equal(N(po).astype(np.int32), C.padding_offset([5, 4, 7, 6], 8))
     assert N(cum).astype(int).tolist() == [0, 5, 9, 16, 22]
+
+
+@pytest.mark.parametrize("cache_dt", [np.float32, np.float16])
+@pytest.mark.parametrize("heads,kvh,lens,hist", [
+    (4, 2, [5, 3, 7], [0, 4, 2]),          # GQA, ragged, history
+    (8, 8, [33, 1, 64, 20], [31, 0, 3, 65]),  # chunks across 32-key blocks, one-token sequence
+    (8, 1, [70], [0]),                     # MQA, one sequence past two query blocks
+])
+def test_context_attention_qkv_fused_matches_oracle(ops, cache_dt, heads, kvh, lens, hist):
+    """llmi_context_attention_qkv (RoPE + the k / v store into the cache + the ragged flash
+    attention, what LLaMAContextAttentionLayer runs for head size 128) against the oracle's
+    composition of the reference's unfused launchers (oracle/context_ops.py:
+    context_attention): the attention output within 1e-5 rel-L2 (fp32 cache) / 1e-4 (fp16
+    cache: both read the same rounded cache; a new k may round to the neighbouring fp16
+    where the two RoPE restatements differ in the last fp32 bit), the new cache
+    slots within 1e-6 (fp32) / one fp16 rounding (fp16), history slots untouched."""
+    rng = np.random.default_rng(len(lens) * 7 + heads)
+    d, layers, layer = 128, 2, 1
+    n, batch, max_q = sum(lens), len(lens), max(lens)
+    max_seq = max(h + q for h, q in zip(hist, lens)) + 5
+    qkv = rng.standard_normal((n, (heads + 2 * kvh) * d)).astype(np.float32)
+    kc = (rng.standard_normal((layers, batch, kvh, max_seq, d)) * 0.5).astype(cache_dt)
+    vc = (rng.standard_normal((layers, batch, kvh, max_seq, d)) * 0.5).astype(cache_dt)
+    ok, ov = kc.copy(), vc.copy()
+    want = C.context_attention(qkv, lens, np.array(hist), heads, kvh, d, ok, ov, layer=layer)
+    po = C.padding_offset(lens, max_q)
+    tdt = torch.float32 if cache_dt == np.float32 else torch.float16
+    tk, tv = T(kc, tdt), T(vc, tdt)
+    got = N(ops.context_attention_qkv(T(qkv), T(po), T(np.array(hist, np.int32)), T(np.array(lens, np.int32)),
+                                      batch, max_q, heads, kvh, tk, tv, layer=layer))
+    e = rel(got, want)
+    print(f"fused context attention heads {heads} kv {kvh} lens {lens} cache {cache_dt.__name__}: rel-L2 {e:.2e}")
+    assert e < (1e-5 if cache_dt == np.float32 else 1e-4)
+    gk, gv = N(tk), N(tv)
+    for b, (h0, q) in enumerate(zip(hist, lens)):
+        np.testing.assert_array_equal(gk[layer, b, :, :h0], kc[layer, b, :, :h0].astype(np.float32))
+        np.testing.assert_array_equal(gv[layer, b, :, :h0], vc[layer, b, :, :h0].astype(np.float32))
+        slot_tol = 1e-6 if cache_dt == np.float32 else 1e-3
+        assert rel(gk[layer, b, :, h0:h0 + q], ok[layer, b, :, h0:h0 + q]) < slot_tol
+        np.testing.assert_array_equal(gv[layer, b, :, h0:h0 + q], ov[layer, b, :, h0:h0 + q].astype(np.float32))
+    np.testing.assert_array_equal(gk[0], kc[0].astype(np.float32))  # other layers untouched
+
+
+@pytest.mark.parametrize("m", [16, 100, 300, 512])
+def test_ffn_fused_matches_fp64(ops, m):
+    """llmi_ffn (gate_up with the SiLU*up epilogue writing the down GEMM's fp16 input planes,
+    then down; gemm2 below 256 rows, gemm3 above) against float64 numpy of
+    W_down (silu(W_gate x) * (W_up x)) with the same fp16 weights: the fp32-faithful planes
+    keep it within 1e-5 rel-L2; an unsupported shape raises instead of launching."""
+    rng = np.random.default_rng(m)
+    hidden, inter = 512, 1024
+    x = rng.standard_normal((m, hidden)).astype(np.float32)
+    wgu = (rng.standard_normal((2 * inter, hidden)) / math.sqrt(hidden)).astype(np.float16)
+    wd = (rng.standard_normal((hidden, inter)) / math.sqrt(inter)).astype(np.float16)
+    got = N(ops.ffn(T(x), T(wgu), T(wd)))
+    x64, g64, d64 = x.astype(np.float64), wgu.astype(np.float64), wd.astype(np.float64)
+    gu = x64 @ g64.T
+    g, u = gu[:, :inter], gu[:, inter:]
+    want = ((g / (1.0 + np.exp(-g))) * u) @ d64.T
+    e = rel(got, want)
+    print(f"fused ffn m {m}: rel-L2 vs fp64 {e:.2e}")
+    assert e < 1e-5
+    from llmi._lib import LlmiError
+    with pytest.raises(LlmiError):
+        ops.ffn(T(x[:8]), T(wgu), T(wd))  # m < 16: the caller's three-launch path
