@@ -307,23 +307,29 @@ def pick_fused_exchange(eng, dist, prompt, world, ref_tokens, n_time: int = 128)
         eng.set_exchange(1)
         out["fused_rejected"] = [o[1] for o in oks if not o[0]][:2]
         return out
-    times = {}
+    times, terr = {}, ""
     n = min(n_time, eng.cfg.max_seq - 1)
-    for m in (1, 2, 1, 2):
-        eng.set_exchange(m)
-        eng.set_prompt(prompt)
-        eng.decode(n)  # graph capture + warm
-        eng.sync()
-        eng.set_prompt(prompt)
-        dist.barrier()
-        t0 = _t.perf_counter()
-        eng.decode(n)
-        eng.sync()
-        dt = _t.perf_counter() - t0
-        times[m] = min(dt, times.get(m, dt))
+    try:  # local work only: no collective may sit inside a block that can raise on one rank
+        for m in (1, 2, 1, 2):
+            eng.set_exchange(m)
+            eng.set_prompt(prompt)
+            eng.decode(n)  # graph capture + warm
+            eng.sync()
+            eng.set_prompt(prompt)
+            t0 = _t.perf_counter()
+            eng.decode(n)
+            eng.sync()
+            dt = _t.perf_counter() - t0
+            times[m] = min(dt, times.get(m, dt))
+    except Exception as e:
+        terr = repr(e)[:300]
     allt = [None] * world
-    dist.all_gather_object(allt, times)
-    worst = {m: max(t[m] for t in allt) for m in (1, 2)}
+    dist.all_gather_object(allt, (times, terr))
+    if any(t[1] or len(t[0]) != 2 for t in allt):
+        eng.set_exchange(1)
+        out["fused_rejected"] = [t[1] for t in allt if t[1]][:2] or ["timing incomplete"]
+        return out
+    worst = {m: max(t[0][m] for t in allt) for m in (1, 2)}
     best = 2 if worst[2] < worst[1] else 1
     eng.set_exchange(best)
     out["mode"] = "fused" if best == 2 else "oneshot"
