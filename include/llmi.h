@@ -98,6 +98,22 @@ int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales
 int llmi_ffn(const float* x, const void* w_gate_up, const void* w_down, int w_dtype, float* y, int m, int hidden,
              int inter, llmi_stream_t stream);
 
+/* The context decoder's projection + residual pair in one call (LlamaContextDecoder,
+ * context_decoder.cpp:104-139): launchLinearGemm(o_proj) followed by
+ * launchFusedAddBiasResidualRMSNorm (no bias), or the FFN followed by launchAddResidual and
+ * the next layer's launchRMSNorm. With p = x . W^T (llmi_linear's arithmetic, K slices summed
+ * in slice order): residual[m, n] += p, then out[m, n] = RMSNorm(residual) * gamma (gamma
+ * null: out = residual; out null: the residual update alone). out may alias x (it is written
+ * after x is read), not residual. fp16 weights, m >= 16, GEMM-tileable n / k, n <= 8192;
+ * other cases return LLMI_EUNSUPPORTED with nothing launched (the caller runs the separate
+ * launches). */
+int llmi_linear_residual(const float* x, const void* w, int w_dtype, int m, int n, int k, float* residual, float* out,
+                         const void* gamma, int gamma_dtype, float eps, llmi_stream_t stream);
+/* llmi_ffn with the same residual epilogue: residual[m, hidden] += FFN(x), then out as above. */
+int llmi_ffn_residual(const float* x, const void* w_gate_up, const void* w_down, int w_dtype, int m, int hidden,
+                      int inter, float* residual, float* out, const void* gamma, int gamma_dtype, float eps,
+                      llmi_stream_t stream);
+
 /* One decode row through the HBM-streaming GEMV with its fused prologue/epilogue -- what
  * LlamaSelfDecoder::forward strings together for a token (self_decoder.cpp:59-81 fused):
  *   gamma != NULL: x is RMS-normalised and scaled by gamma (dtype gamma_dtype) first;

@@ -506,27 +506,15 @@ public:
         TensorWrapper<int>* layer_id = inputs["layer_id"]->as<int>();
         llmi_detail::ActF32 in(inputs["attention_input"], allocator, stream, true, "LLaMAContextAttentionLayer");
         llmi_detail::ActF32 out(outputs["attention_output"], allocator, stream, false, "LLaMAContextAttentionLayer");
-        // 1. qkv linear
-        launchLinearGemm(in.get(), weights.qkv, qkv_buf_wo_pad, c, false, true);
-        const int max_seq = outputs["all_k_cache"]->shape[3];
-        void* kcache = cdt == FP32 ? (void*)outputs["all_k_cache"]->as<float>()->data
-                                   : (void*)outputs["all_k_cache"]->as<half_t>()->data;
-        void* vcache = cdt == FP32 ? (void*)outputs["all_v_cache"]->as<float>()->data
-                                   : (void*)outputs["all_v_cache"]->as<half_t>()->data;
         if (fused()) {
-            // 2-5 fused: RoPE with the k / v rows stored straight into the cache after the
-            // history, then the attention core over the cache (one launch each; fp16 caches
-            // are read as they are: the unfused chain widens exactly these values to fp32)
-            LLMI_CALL(llmi_context_attention_qkv(
-                qkv_buf_wo_pad->data, padding_offset->data, history_length->data, input_length->data, params.num_tokens,
-                params.batch_size, params.max_q_len, head_num, kv_head_num, head_size,
-                static_params.rotary_embedding_base, kcache, vcache, cdt == FP32 ? LLMI_F32 : LLMI_F16,
-                layer_id->getVal(), max_seq, scale, q_buf_w_pad->data, qkv_buf_wo_pad_1->data, stream));
-            launchLinearGemm(qkv_buf_wo_pad_1, weights.output, out.get(), c, false, true);
+            launchLinearGemm(forwardCore(in.get(), inputs, outputs, weights, params, static_params), weights.output,
+                             out.get(), c, false, true);
             out.store();
             freeBuf();
             return;
         }
+        // 1. qkv linear
+        launchLinearGemm(in.get(), weights.qkv, qkv_buf_wo_pad, c, false, true);
         // 2. RoPE (position history + s) and [num_tokens, ...] -> [bs, heads, max_q_len, head]
         launchAddFusedQKVBiasTransposeAndRoPE(q_buf_w_pad, k_buf_w_pad, v_buf_w_pad, qkv_buf_wo_pad, weights.qkv,
                                               padding_offset, history_length, input_length, static_params, stream);
@@ -569,6 +557,31 @@ public:
         launchLinearGemm(qkv_buf_wo_pad_1, weights.output, out.get(), c, false, true);
         out.store();
         freeBuf();
+    }
+
+    // forward's steps 1-5 without o_proj, fused core only (fused(), after allocForForward):
+    // qkv projection of x (fp32 [num_tokens, H]), then RoPE with the k / v rows stored
+    // straight into the cache after the history, then the attention core over the cache (one
+    // launch each; fp16 caches are read as they are: the unfused chain widens exactly these
+    // values to fp32). Returns the [num_tokens, H] attention rows, valid until freeBuf().
+    TensorWrapper<float>* forwardCore(TensorWrapper<float>* x, TensorMap& inputs, TensorMap& outputs,
+                                      LLaMAattentionWeights<T>& weights, LLaMAAttentionDynParams& params,
+                                      LLaMAAttentionStaticParams& static_params) {
+        LLM_CHECK_WITH_INFO(fused() && qkv_buf_wo_pad_1, "forwardCore: fused core after allocForForward only");
+        const DataType cdt = outputs["all_k_cache"]->dtype;
+        cublasWrapper cw{stream};
+        launchLinearGemm(x, weights.qkv, qkv_buf_wo_pad, cublas_wrapper ? cublas_wrapper : &cw, false, true);
+        void* kcache = cdt == FP32 ? (void*)outputs["all_k_cache"]->as<float>()->data
+                                   : (void*)outputs["all_k_cache"]->as<half_t>()->data;
+        void* vcache = cdt == FP32 ? (void*)outputs["all_v_cache"]->as<float>()->data
+                                   : (void*)outputs["all_v_cache"]->as<half_t>()->data;
+        LLMI_CALL(llmi_context_attention_qkv(
+            qkv_buf_wo_pad->data, inputs["padding_offset"]->as<int>()->data, inputs["history_length"]->as<int>()->data,
+            inputs["input_length"]->as<int>()->data, params.num_tokens, params.batch_size, params.max_q_len, head_num,
+            kv_head_num, head_size, static_params.rotary_embedding_base, kcache, vcache,
+            cdt == FP32 ? LLMI_F32 : LLMI_F16, inputs["layer_id"]->as<int>()->getVal(),
+            outputs["all_k_cache"]->shape[3], scale, q_buf_w_pad->data, qkv_buf_wo_pad_1->data, stream));
+        return qkv_buf_wo_pad_1;
     }
 
 private:
@@ -665,9 +678,20 @@ public:
                                   {"all_v_cache", output_tensors["all_v_cache"]}};
         TensorMap ffn_inputs{{"ffn_input", decoder_output}}, ffn_outputs{{"ffn_output", decoder_output}};
         dyn_params.is_ctx = true;  // FFN scratch of num_tokens rows
+        LLM_CHECK_WITH_INFO((int)layerWeights.size() >= num_layer, "LlamaContextDecoder: fewer layer weights than layers");
+        const bool fast = ctxAttn.fused();
+        if (fast) launchRMSNorm(din.get(), decoder_residual.get(), layerWeights[0]->attn_norm_weight, rmsnorm_eps, false,
+                                stream);
+        fuse_o = fuse_f = true;
         for (layer = 0; layer < num_layer; ++layer) {
             LlamaLayerWeight<T>* w = layerWeights[layer];
             TensorWrapper<float>* decoder_input = ctx_attn_inputs["attention_input"]->as<float>();
+            if (fast) {
+                fast_layer(decoder_input, decoder_output, ctx_attn_inputs, ctx_attn_output, w,
+                           layer + 1 < num_layer ? layerWeights[layer + 1] : nullptr, dyn_params);
+                ctx_attn_inputs.insert("attention_input", decoder_output);
+                continue;
+            }
             launchRMSNorm(decoder_input, decoder_residual.get(), w->attn_norm_weight, rmsnorm_eps, false, stream);
             ctxAttn.forward(ctx_attn_inputs, ctx_attn_output, w->self_attn_weight, dyn_params,
                             ctxAttn.GetAttnStaticParams());
@@ -683,12 +707,58 @@ public:
     }
 
 private:
+    // One layer with the fused attention core and each projection + residual pair as one call
+    // (llmi_linear_residual: o_proj + launchFusedAddBiasResidualRMSNorm; llmi_ffn_residual: the
+    // FFN + launchAddResidual + the next layer's launchRMSNorm). Each falls back to those
+    // separate launches when it returns LLMI_EUNSUPPORTED (fp32 weights, small batches).
+    // Invariant entering a layer: residual = x_l, xn = RMSNorm(x_l) * attn_norm_l; leaving it,
+    // the same for l + 1 in y (the last layer: y = x_L, the reference's decoder output).
+    void fast_layer(TensorWrapper<float>* xn, TensorWrapper<float>* y, TensorMap& ain, TensorMap& aout,
+                    LlamaLayerWeight<T>* w, LlamaLayerWeight<T>* next, LLaMAAttentionDynParams& p) {
+        const int wdt = llmiWeightDtype(getWeightType<T>());
+        const int rows = p.num_tokens, H = hidden_units, inter = w->ffn_weight.down.shape[1];
+        float* r = decoder_residual->data;
+        ctxAttn.allocForForward(p);
+        TensorWrapper<float>* a = ctxAttn.forwardCore(xn, ain, aout, w->self_attn_weight, p,
+                                                      ctxAttn.GetAttnStaticParams());
+        // r += a . Wo^T; y = RMSNorm(r) * ffn_norm
+        int rc = fuse_o ? llmi_linear_residual(a->data, w->self_attn_weight.output.data, wdt, rows, H, H, r, y->data,
+                                               w->ffn_norm_weight.gamma, wdt, rmsnorm_eps, stream)
+                        : LLMI_EUNSUPPORTED;
+        if (rc == LLMI_EUNSUPPORTED) {
+            fuse_o = false;
+            cublasWrapper cw{stream};
+            launchLinearGemm(a, w->self_attn_weight.output, y, &cw, false, true);
+            BaseWeight<T> no_bias;
+            launchFusedAddBiasResidualRMSNorm(decoder_residual.get(), y, no_bias, w->ffn_norm_weight.gamma, rmsnorm_eps,
+                                              stream);
+        } else {
+            LLMI_CALL(rc);
+        }
+        ctxAttn.freeBuf();
+        // r += FFN(y); y = RMSNorm(r) * the next layer's attn_norm (after the last layer: y = r)
+        rc = fuse_f ? llmi_ffn_residual(y->data, w->ffn_weight.gateAndup.data, w->ffn_weight.down.data, wdt, rows, H,
+                                        inter, r, y->data, next ? next->attn_norm_weight.gamma : nullptr, wdt,
+                                        rmsnorm_eps, stream)
+                    : LLMI_EUNSUPPORTED;
+        if (rc == LLMI_EUNSUPPORTED) {
+            fuse_f = false;
+            TensorMap fi{{"ffn_input", y}}, fo{{"ffn_output", y}};
+            ffn.forward(fi, fo, w->ffn_weight, p);
+            launchAddResidual(decoder_residual.get(), y, false, stream);
+            if (next) launchRMSNorm(y, decoder_residual.get(), next->attn_norm_weight, rmsnorm_eps, false, stream);
+        } else {
+            LLMI_CALL(rc);
+        }
+    }
+
     int hidden_units, num_layer;
     float rmsnorm_eps;
     void* stream;
     BaseAllocator* allocator;
     LLaMAContextAttentionLayer<T> ctxAttn;
     LLaMAFFNLayer<T> ffn;
+    bool fuse_o = true, fuse_f = true;
     float *mask_ptr = nullptr, *resid_ptr = nullptr;
     int *po_ptr = nullptr, *cum_ptr = nullptr;
     std::unique_ptr<TensorWrapper<float>> attention_mask, decoder_residual;

@@ -64,6 +64,46 @@ int llmi_ffn(const float* x, const void* w_gate_up, const void* w_down, int w_dt
     return ffn_mfma_launch(x, w_gate_up, w_down, y, m, hidden, inter, STREAM(stream));
 }
 
+namespace {
+bool resid_args_ok(const float* x, const void* w, int w_dtype, float* residual, float* out, const void* gamma,
+                   int gamma_dtype, int n) {
+    auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    return w_dtype == LLMI_F16 && a16(x) && a16(w) && a16(residual) && a16(out) && n % 4 == 0 && n <= 8192 &&
+           (!gamma || gamma_dtype == LLMI_F16 || gamma_dtype == LLMI_F32);
+}
+}  // namespace
+
+int llmi_linear_residual(const float* x, const void* w, int w_dtype, int m, int n, int k, float* residual, float* out,
+                         const void* gamma, int gamma_dtype, float eps, llmi_stream_t stream) {
+    LLMI_REQUIRE(x && w && residual && m >= 1 && n >= 1 && k >= 1, "linear_residual: bad arguments");
+    LLMI_REQUIRE(out != residual, "linear_residual: out must not alias the residual");
+    if (!resid_args_ok(x, w, w_dtype, residual, out, gamma, gamma_dtype, n) || !linear_mfma_supported(m, n, k)) {
+        set_last_error("[llmi][ERROR] linear_residual: needs fp16 weights, M >= 16, GEMM-tileable n / k, n <= 8192 "
+                       "and 16-B aligned buffers (use llmi_linear + llmi_add_residual_rmsnorm)");
+        return LLMI_EUNSUPPORTED;
+    }
+    ResidEpi re;
+    re.resid = residual; re.out = out; re.gamma = gamma; re.g_dtype = gamma ? gamma_dtype : LLMI_F32; re.eps = eps;
+    return linear_mfma_launch(x, w, nullptr, m, n, k, STREAM(stream), &re);
+}
+
+int llmi_ffn_residual(const float* x, const void* w_gate_up, const void* w_down, int w_dtype, int m, int hidden,
+                      int inter, float* residual, float* out, const void* gamma, int gamma_dtype, float eps,
+                      llmi_stream_t stream) {
+    LLMI_REQUIRE(x && w_gate_up && w_down && residual && m >= 1 && hidden >= 1 && inter >= 1,
+                 "ffn_residual: bad arguments");
+    LLMI_REQUIRE(out != residual, "ffn_residual: out must not alias the residual");
+    if (!resid_args_ok(x, w_gate_up, w_dtype, residual, out, gamma, gamma_dtype, hidden) ||
+        (reinterpret_cast<uintptr_t>(w_down) & 15) || !ffn_mfma_supported(m, hidden, inter)) {
+        set_last_error("[llmi][ERROR] ffn_residual: needs fp16 weights, M >= 16, GEMM-tileable hidden / inter, "
+                       "hidden <= 8192 and 16-B aligned buffers (use llmi_ffn + llmi_add_residual)");
+        return LLMI_EUNSUPPORTED;
+    }
+    ResidEpi re;
+    re.resid = residual; re.out = out; re.gamma = gamma; re.g_dtype = gamma ? gamma_dtype : LLMI_F32; re.eps = eps;
+    return ffn_mfma_launch(x, w_gate_up, w_down, nullptr, m, hidden, inter, STREAM(stream), &re);
+}
+
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
                 llmi_stream_t stream) {
     LLMI_REQUIRE(m >= 1 && n >= 1 && k >= 1, "linear: m, n, k must be >= 1");

@@ -445,6 +445,76 @@ __global__ __launch_bounds__(kThreads) void slab_sum_kernel(const float4* slab, 
         y[i] = a;
     }
 }
+// ResidEpi (kernels.h), one workgroup per row: t = slice 0 + slice 1 + ... (slab_sum_kernel's
+// order), r = resid + t (add_resid_rmsnorm_kernel's / add_resid_kernel's order), then the
+// row's RMSNorm * gamma -- the launchLinearGemm + launchFusedAddBiasResidualRMSNorm pair
+// (or + launchAddResidual + the next layer's launchRMSNorm) in one pass over the slices.
+template <int NPT>
+__global__ __launch_bounds__(kThreads) void resid_norm_kernel(float* resid, const float* slab, int ks, int m, int n,
+                                                              float* out, const void* gamma, int g_dtype, float eps) {
+    __shared__ float red[16];
+    const size_t row = blockIdx.x;
+    const int n4 = n / 4;
+    const size_t plane4 = (size_t)m * n4;
+    const float4* sl = reinterpret_cast<const float4*>(slab) + row * n4;
+    float4* rr = reinterpret_cast<float4*>(resid) + row * n4;
+    float4 v[NPT];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+        const int j = threadIdx.x + i * kThreads;
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j >= n4) continue;
+        float4 t = sl[j];
+        for (int s = 1; s < ks; ++s) {
+            const float4 b = sl[(size_t)s * plane4 + j];
+            t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
+        }
+        const float4 r = rr[j];
+        v[i] = make_float4(r.x + t.x, r.y + t.y, r.z + t.z, r.w + t.w);
+        rr[j] = v[i];
+        ss += v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
+    }
+    if (!out) return;
+    float rstd = 1.f;
+    if (gamma) {
+        ss = block_sum(ss, red);
+        rstd = 1.0f / sqrtf(ss / (float)n + eps);
+    }
+    float4* o = reinterpret_cast<float4*>(out) + row * n4;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+        const int j = threadIdx.x + i * kThreads;
+        if (j >= n4) continue;
+        float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        if (gamma) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float g = g_dtype == LLMI_F16 ? __half2float(static_cast<const __half*>(gamma)[4 * j + q])
+                                                    : static_cast<const float*>(gamma)[4 * j + q];
+                e[q] = g * (e[q] * rstd);
+            }
+        }
+        o[j] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+}
+int resid_norm_launch(const ResidEpi& re, const float* slab, int ks, int m, int n, hipStream_t s) {
+    const int npt = (n / 4 + kThreads - 1) / kThreads;
+    if (npt <= 4)
+        hipLaunchKernelGGL(resid_norm_kernel<4>, dim3(m), dim3(kThreads), 0, s, re.resid, slab, ks, m, n, re.out,
+                           re.gamma, re.g_dtype, re.eps);
+    else
+        hipLaunchKernelGGL(resid_norm_kernel<8>, dim3(m), dim3(kThreads), 0, s, re.resid, slab, ks, m, n, re.out,
+                           re.gamma, re.g_dtype, re.eps);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+bool resid_epi_ok(const ResidEpi* re, int n) {
+    return !re || (re->resid && n % 4 == 0 && n <= 8 * 4 * kThreads &&
+                   (reinterpret_cast<uintptr_t>(re->resid) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(re->out) & 15) == 0 &&
+                   (re->g_dtype == LLMI_F16 || re->g_dtype == LLMI_F32));
+}
 // keyed by (device, stream): the null stream is the same handle on every device
 std::mutex g_ws_mu;
 std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> g_ws;
@@ -477,10 +547,14 @@ bool linear_mfma_supported(int m, int n, int k) {
     return m >= 16 && k % 64 == 0 && gemm2_supported(n, k, EPI_STORE);
 }
 
-int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s) {
-    LLMI_REQUIRE(x && w && y && linear_mfma_supported(m, n, k), "linear_mfma: N a multiple of 128, K of 64, M >= 16");
+int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s,
+                       const ResidEpi* re) {
+    LLMI_REQUIRE(x && w && (y || re) && linear_mfma_supported(m, n, k),
+                 "linear_mfma: N a multiple of 128, K of 64, M >= 16");
     LLMI_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
                  "linear_mfma: x and y must be 16-B aligned");
+    LLMI_REQUIRE(resid_epi_ok(re, n), "linear_mfma: residual epilogue needs n <= 8192 (multiple of 4), 16-B aligned "
+                                      "residual / out and an fp16 or fp32 gamma");
     const bool g3 = m >= 256 && gemm3_supported(n, k, EPI_STORE, 1);
     const int tiles = g3 ? ((m + 255) / 256) * (n / 256) : ((m + 127) / 128) * (n / kBN);
     int ks = 1;  // K slices while the tiles leave more than a third of the 256 CUs idle
@@ -490,7 +564,7 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
         ks = nk;
     }
     const size_t plane = ((size_t)m * k * 2 + 255) / 256 * 256;
-    const size_t slab = ks > 1 ? (size_t)ks * m * n * 4 : 0;
+    const size_t slab = ks > 1 || re ? (size_t)ks * m * n * 4 : 0;  // the residual form: always (>= 1) slices
     char* ws = nullptr;
     LLMI_TRY(linear_workspace(s, 2 * plane + slab, &ws));
     _Float16* hi = reinterpret_cast<_Float16*>(ws);
@@ -502,12 +576,14 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
     Gemm2Args g;
     g.a[0] = hi; g.a[1] = lo; g.planes = 2; g.lda = k;
     g.w = w; g.m = m; g.n = n; g.k = k; g.ldy = n;
+    float* sl = reinterpret_cast<float*>(ws + 2 * plane);
     if (ks > 1) {
-        g.epi = EPI_SLAB; g.ksplit = ks; g.slab = reinterpret_cast<float*>(ws + 2 * plane); g.y = y;
+        g.epi = EPI_SLAB; g.ksplit = ks; g.slab = sl; g.y = re ? sl : y;
     } else {
-        g.epi = EPI_STORE; g.y = y;
+        g.epi = EPI_STORE; g.y = re ? sl : y;
     }
     LLMI_TRY(g3 ? gemm3_launch(g, s) : gemm2_launch(g, s));
+    if (re) return resid_norm_launch(*re, sl, ks, m, n, s);
     if (ks > 1) {
         const size_t n4y = (size_t)m * n / 4;
         hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_of(n4y)), dim3(kThreads), 0, s,
@@ -529,11 +605,13 @@ bool ffn_mfma_supported(int m, int hidden, int inter) {
 }
 
 int ffn_mfma_launch(const float* x, const void* w_gu, const void* w_down, float* y, int m, int hidden, int inter,
-                    hipStream_t s) {
-    LLMI_REQUIRE(x && w_gu && w_down && y && ffn_mfma_supported(m, hidden, inter),
+                    hipStream_t s, const ResidEpi* re) {
+    LLMI_REQUIRE(x && w_gu && w_down && (y || re) && ffn_mfma_supported(m, hidden, inter),
                  "ffn_mfma: unsupported shape (M >= 16, hidden and inter multiples of 64 the GEMMs tile)");
     LLMI_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
                  "ffn_mfma: x and y must be 16-B aligned");
+    LLMI_REQUIRE(resid_epi_ok(re, hidden), "ffn_mfma: residual epilogue needs hidden <= 8192 (multiple of 4), 16-B "
+                                           "aligned residual / out and an fp16 or fp32 gamma");
     const bool g3gu = m >= 256 && gemm3_supported(2 * inter, hidden, EPI_SILU_MUL, 1);
     const bool g3d = m >= 256 && gemm3_supported(hidden, inter, EPI_STORE, 1);
     const int tiles = g3d ? ((m + 255) / 256) * (hidden / 256) : ((m + 127) / 128) * (hidden / kBN);
@@ -545,7 +623,7 @@ int ffn_mfma_launch(const float* x, const void* w_gu, const void* w_down, float*
     }
     const size_t xplane = ((size_t)m * hidden * 2 + 255) / 256 * 256;
     const size_t aplane = ((size_t)m * inter * 2 + 255) / 256 * 256;
-    const size_t slab = ks > 1 ? (size_t)ks * m * hidden * 4 : 0;
+    const size_t slab = ks > 1 || re ? (size_t)ks * m * hidden * 4 : 0;
     char* ws = nullptr;
     LLMI_TRY(linear_workspace(s, 2 * xplane + 2 * aplane + slab, &ws));
     _Float16* xh = reinterpret_cast<_Float16*>(ws);
@@ -564,12 +642,14 @@ int ffn_mfma_launch(const float* x, const void* w_gu, const void* w_down, float*
     Gemm2Args d;
     d.a[0] = ah; d.a[1] = al; d.planes = 2; d.lda = inter;
     d.w = w_down; d.m = m; d.n = hidden; d.k = inter; d.ldy = hidden;
+    float* sl = reinterpret_cast<float*>(ws + 2 * xplane + 2 * aplane);
     if (ks > 1) {
-        d.epi = EPI_SLAB; d.ksplit = ks; d.slab = reinterpret_cast<float*>(ws + 2 * xplane + 2 * aplane); d.y = y;
+        d.epi = EPI_SLAB; d.ksplit = ks; d.slab = sl; d.y = re ? sl : y;
     } else {
-        d.epi = EPI_STORE; d.y = y;
+        d.epi = EPI_STORE; d.y = re ? sl : y;
     }
     LLMI_TRY(g3d ? gemm3_launch(d, s) : gemm2_launch(d, s));
+    if (re) return resid_norm_launch(*re, sl, ks, m, hidden, s);
     if (ks > 1) {
         const size_t n4y = (size_t)m * hidden / 4;
         hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_of(n4y)), dim3(kThreads), 0, s,

@@ -140,8 +140,18 @@ int w8_prepare(const void* w16, int rows, int cols, void* w8, int* exp_out, hipS
 bool gemm2_supported(int n, int k, int epi);
 // the context FFN (gate_up + SiLU*up + down) on the matrix cores, fp16 weights (gemm2.hip)
 bool ffn_mfma_supported(int m, int hidden, int inter);
+// residual epilogue of llmi_linear_residual / llmi_ffn_residual: resid += the projection
+// (its K slices summed in slice order first), then out = gamma ? RMSNorm(resid) * gamma
+// : resid (out null: the residual update alone); n <= 8192, a multiple of 4
+struct ResidEpi {
+    float* resid = nullptr;
+    float* out = nullptr;
+    const void* gamma = nullptr;
+    int g_dtype = 0;
+    float eps = 0.f;
+};
 int ffn_mfma_launch(const float* x, const void* w_gu, const void* w_down, float* y, int m, int hidden, int inter,
-                    hipStream_t s);
+                    hipStream_t s, const ResidEpi* re = nullptr);
 int gemm2_launch(Gemm2Args a, hipStream_t s);
 // the same GEMM on 256 x 256 tiles with a ping-pong 8-wave schedule (gemm3.hip)
 bool gemm3_supported(int n, int k, int epi, int ksplit);
@@ -149,7 +159,8 @@ int gemm3_launch(Gemm2Args a, hipStream_t s);
 // llmi_linear for fp16 weights (the layer API's projections): fp32 x split into planes,
 // then gemm3 / gemm2 (+ split-K slices summed in order); see gemm2.hip
 bool linear_mfma_supported(int m, int n, int k);
-int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s);
+int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s,
+                       const ResidEpi* re = nullptr);
 // rows of x (+= the ksplit slices of slab, in slice order, written back to x),
 // then optional RMSNorm, then fp16 planes hi[, lo] (hi null: the combine alone)
 int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,

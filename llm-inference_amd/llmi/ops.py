@@ -271,6 +271,33 @@ def ffn(x, w_gate_up, w_down):
     return y
 
 
+def linear_residual(x, w, residual, gamma=None, eps: float = 1e-5, out: bool = True):
+    """llmi_linear_residual: residual += x . w^T (in place), then returns RMSNorm(residual) *
+    gamma (gamma None: a copy of the residual; out False: None). x [m, k] fp32, w [n, k] fp16,
+    residual [m, n] fp32, gamma [n] fp16 / fp32."""
+    _dev(x, w, residual)
+    m, k = x.shape
+    n = w.shape[0]
+    y = torch.empty(m, n, device=x.device, dtype=torch.float32) if out else None
+    call("llmi_linear_residual", x.contiguous().data_ptr(), w.data_ptr(), _dt(w), m, n, k, residual.data_ptr(),
+         y.data_ptr() if out else None, gamma.data_ptr() if gamma is not None else None,
+         _dt(gamma) if gamma is not None else 0, float(eps), _stream())
+    return y
+
+
+def ffn_residual(x, w_gate_up, w_down, residual, gamma=None, eps: float = 1e-5, out: bool = True):
+    """llmi_ffn_residual: residual += FFN(x) (in place), then the output as linear_residual."""
+    _dev(x, w_gate_up, w_down, residual)
+    m, hidden = x.shape
+    inter = w_down.shape[1]
+    y = torch.empty(m, hidden, device=x.device, dtype=torch.float32) if out else None
+    call("llmi_ffn_residual", x.contiguous().data_ptr(), w_gate_up.data_ptr(), w_down.data_ptr(), _dt(w_gate_up), m,
+         hidden, inter, residual.data_ptr(), y.data_ptr() if out else None,
+         gamma.data_ptr() if gamma is not None else None, _dt(gamma) if gamma is not None else 0, float(eps),
+         _stream())
+    return y
+
+
 def launchLinearStridedBatchGemm(input1, input2, trans_a: bool = False, trans_b: bool = False):
     """input1 [bs, heads, m|k, k|m], input2 [bs, heads, k|n, n|k] -> [bs, heads, m, n] =
     op(input1) @ op(input2) (linear.cu:126-229; QK^T with trans_b, PV without)."""

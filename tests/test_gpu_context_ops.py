@@ -319,3 +319,72 @@ def test_ffn_fused_matches_fp64(ops, m):
     from llmi._lib import LlmiError
     with pytest.raises(LlmiError):
         ops.ffn(T(x[:8]), T(wgu), T(wd))  # m < 16: the caller's three-launch path
+
+
+@pytest.mark.parametrize("m", [16, 300, 512])
+@pytest.mark.parametrize("gdt", [np.float16, np.float32])
+def test_linear_residual_matches_composition(ops, m, gdt):
+    """llmi_linear_residual (o_proj + launchFusedAddBiasResidualRMSNorm as one call; the
+    residual epilogue sums the K slices in slice order, then adds the residual) against the
+    separate launches on the same inputs: the updated residual is bit-identical (same
+    additions in the same order), the normalised rows within 1e-6 rel-L2 (the row's sum of
+    squares is reduced in another order); gamma None returns the residual, out False only
+    updates it; an unsupported shape raises before launching. K 2048 at 512 rows takes the
+    8-slice split."""
+    rng = np.random.default_rng(m)
+    n, k, eps = 512, 2048, 1e-5
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    w = (rng.standard_normal((n, k)) / math.sqrt(k)).astype(np.float16)
+    r0 = rng.standard_normal((m, n)).astype(np.float32)
+    gamma = (1.0 + 0.1 * rng.standard_normal(n)).astype(gdt)
+    r = T(r0)
+    y = ops.linear_residual(T(x), T(w), r, T(gamma), eps)
+    r_ref, y_ref = T(r0), ops.launchLinearGemm(T(x), T(w))
+    ops.launchFusedAddBiasResidualRMSNorm(r_ref, y_ref, T(gamma), eps)
+    np.testing.assert_array_equal(N(r), N(r_ref))
+    e = rel(N(y), N(y_ref))
+    print(f"linear_residual m {m} gamma {np.dtype(gdt).name}: normalised rows rel-L2 vs separate launches {e:.2e}")
+    assert e < 1e-6
+    # float64 restatement of the pair (the projection's own error bar: llmi_linear's 1e-5)
+    r64 = r0.astype(np.float64) + x.astype(np.float64) @ w.astype(np.float64).T
+    assert rel(N(r), r64) < 1e-5
+    r2 = T(r0)
+    copy = ops.linear_residual(T(x), T(w), r2, None, eps)
+    np.testing.assert_array_equal(N(copy), N(r2))
+    r3 = T(r0)
+    assert ops.linear_residual(T(x), T(w), r3, T(gamma), eps, out=False) is None
+    np.testing.assert_array_equal(N(r3), N(r_ref))
+    from llmi._lib import LlmiError
+    with pytest.raises(LlmiError):
+        ops.linear_residual(T(x[:8]), T(w), T(r0[:8]), T(gamma), eps)  # m < 16
+
+
+@pytest.mark.parametrize("m", [16, 300, 512])
+def test_ffn_residual_matches_composition(ops, m):
+    """llmi_ffn_residual (the FFN + launchAddResidual + the next layer's launchRMSNorm as one
+    call) against llmi_ffn followed by those launches: residual bit-identical, normalised
+    rows within 1e-6 rel-L2, and within 1e-5 of float64."""
+    rng = np.random.default_rng(100 + m)
+    hidden, inter, eps = 512, 1024, 1e-6
+    x = rng.standard_normal((m, hidden)).astype(np.float32)
+    wgu = (rng.standard_normal((2 * inter, hidden)) / math.sqrt(hidden)).astype(np.float16)
+    wd = (rng.standard_normal((hidden, inter)) / math.sqrt(inter)).astype(np.float16)
+    r0 = rng.standard_normal((m, hidden)).astype(np.float32)
+    gamma = (1.0 + 0.1 * rng.standard_normal(hidden)).astype(np.float16)
+    r = T(r0)
+    xt = T(x)
+    y = ops.ffn_residual(xt, T(wgu), T(wd), r, T(gamma), eps)
+    f = ops.ffn(T(x), T(wgu), T(wd))
+    ops.launchAddResidual(T(r0), f)  # f = r0 + ffn(x): the next layer's input
+    np.testing.assert_array_equal(N(r), N(f))
+    r_ref = torch.empty_like(f)
+    ops.launchRMSNorm(f, T(gamma), eps, r_ref)
+    e = rel(N(y), N(f))
+    print(f"ffn_residual m {m}: normalised rows rel-L2 vs separate launches {e:.2e}")
+    assert e < 1e-6
+    x64, g64, d64 = x.astype(np.float64), wgu.astype(np.float64), wd.astype(np.float64)
+    gu = x64 @ g64.T
+    g, u = gu[:, :inter], gu[:, inter:]
+    r64 = r0.astype(np.float64) + ((g / (1.0 + np.exp(-g))) * u) @ d64.T
+    assert rel(N(r), r64) < 1e-5
+    np.testing.assert_array_equal(N(xt), x)  # x read, never written (out is a new tensor here)
