@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "xchg_impl.h"
 #include "prng.h"
 
 namespace llmi {
@@ -145,7 +146,8 @@ struct Engine {
     // xchg_mode 2 moves the exchange into the producing launches (o_proj, down, lm_head
     // finish with xchg_tail: push + wait + reduce, no exchange launch). tail_mode: what
     // those launches do (0 nothing, 1 push only -- the in-process group, 3 push + reduce);
-    // xt_cnt their arrival counter pair (zeroed here, reset by each launch's last tail).
+    // xt_cnt their arrival counters (xchg_impl.h: sharded, zeroed here, re-zeroed by every
+    // fused launch's finishers).
     int xchg_mode = 0;
     int tail_mode = 0;
     unsigned* xt_cnt = nullptr;
@@ -739,8 +741,8 @@ struct Engine {
         LLMI_HIP(hipMalloc(&xchg_ep, kXchgMaxSlices * sizeof(unsigned long long)));
         LLMI_HIP(hipMemset(xchg_ep, 0, kXchgMaxSlices * sizeof(unsigned long long)));
         LLMI_HIP(hipMalloc(&peers_dev, (size_t)W * sizeof(char*)));
-        LLMI_HIP(hipMalloc(&xt_cnt, 64));
-        LLMI_HIP(hipMemset(xt_cnt, 0, 64));
+        LLMI_HIP(hipMalloc(&xt_cnt, xchg_detail::kTailWords * sizeof(unsigned)));
+        LLMI_HIP(hipMemset(xt_cnt, 0, xchg_detail::kTailWords * sizeof(unsigned)));
         return LLMI_OK;
     }
     // every rank's inbox base, in rank order (peers[rank] must be this rank's own inbox)

@@ -343,7 +343,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
         if (tid == 0) {
             unsigned long long b = best_s[0];
             for (int i = 1; i < kWavesPerBlock; ++i) b = best_s[i] > b ? best_s[i] : b;
-            a.partials[bid] = b;
+            // agent-scope (write-through) store: a fused exchange tail may read it in-launch
+            __hip_atomic_store(a.partials + bid, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

@@ -91,32 +91,48 @@ __device__ __forceinline__ void reduce_slice(const XchgArgs& a, int g, unsigned 
 }
 
 // The producer-fused exchange: called by EVERY thread of EVERY workgroup of a kernel whose
-// workgroups produced a.buf (int64 atomics or stores), after their last write. Each
-// workgroup drains its writes, releases them (agent scope) and takes an arrival ticket;
-// the last m = min(grid, slices) to arrive wait for the grid's last arrival, then each
-// pushes (a.mode & 1) and reduces (a.mode & 2) slices j, j + m, ... The counter pair
-// cnt[0..1] (zeroed at allocation) is reset by the last tail workgroup to finish, so the
-// next fused launch on the stream finds it zero. lds: one int of LDS scratch.
+// workgroups produced a.buf with device-scope atomics or agent-scope (sc1) stores -- both
+// land at the point of coherence, so a drained workgroup needs no release fence (an agent
+// release per workgroup, i.e. an L2 write-back from each of up to ~1000 workgroups, cost
+// ~18 us per launch in the first version; so did a single arrival counter, whose
+// same-address atomics serialise at ~10 ns each). Arrivals are counted on kTailShards
+// counters (workgroup b -> shard b % S, one 128-B line each); the workgroup that completes
+// its shard re-zeroes that shard (all of its members have arrived) and takes a ticket on
+// the top counter. These S shard finishers wait for the top counter to reach S, then
+// finisher g pushes (a.mode & 1) and reduces (a.mode & 2) slices g, g + S, ... The last
+// finisher to leave re-zeroes the top pair, so the next fused launch on the stream finds
+// every word zero (they are zeroed once at allocation). lds: one int of LDS scratch.
 // Waits are bounded (error bit 8), so a lost peer ends the run with an error, never a hang.
+constexpr int kTailShards = 32;
+constexpr int kTailStride = 32;  // words between counters (128 B)
+constexpr int kTailWords = (kTailShards + 2) * kTailStride;  // shards, then top, then done
 __device__ __forceinline__ void xchg_tail(const XchgArgs& a, unsigned* cnt, int* lds) {
     if (a.buf == nullptr) return;
     const int G = (int)(gridDim.x * gridDim.y * gridDim.z);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's atomics / stores done
+    const int b = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    const int S = G < kTailShards ? G : kTailShards;
+    const int sh = b % S;
+    const int members = G / S + (sh < G % S ? 1 : 0);
+    unsigned* shard = cnt + sh * kTailStride;
+    unsigned* top = cnt + kTailShards * kTailStride;
+    unsigned* done = top + kTailStride;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's atomics / sc1 stores landed
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        *lds = (int)__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int g = -1;
+        if (__hip_atomic_fetch_add(shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1) {
+            __hip_atomic_store(shard, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g = (int)__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *lds = g;
     }
     __syncthreads();
-    const int t = *lds;
-    const int ns = (a.n + kXchgSlice - 1) / kXchgSlice;
-    const int m = min(G, ns);
-    if (t < G - m) return;
-    if (threadIdx.x == 0) {  // the grid's last arrival (the other tail workgroups are already resident)
+    const int g = *lds;
+    if (g < 0) return;
+    if (threadIdx.x == 0) {  // every shard complete (the other finishers are resident: they are running)
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         for (unsigned it = 0;; ++it) {
-            if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)G) break;
+            if (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)S) break;
             if ((it & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
                 atomicOr(a.err, 8);
                 break;
@@ -126,17 +142,18 @@ __device__ __forceinline__ void xchg_tail(const XchgArgs& a, unsigned* cnt, int*
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
-    for (int g = t - (G - m); g < ns; g += m) {
-        const unsigned long long e = a.ep[g] + 1;
-        if (a.mode & 1) push_slice<true>(a, g, e);
-        if (a.mode & 2) reduce_slice(a, g, e);
+    const int ns = (a.n + kXchgSlice - 1) / kXchgSlice;
+    for (int sl = g; sl < ns; sl += S) {
+        const unsigned long long e = a.ep[sl] + 1;
+        if (a.mode & 1) push_slice<true>(a, sl, e);
+        if (a.mode & 2) reduce_slice(a, sl, e);
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const unsigned d = __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == (unsigned)m - 1) {  // every tail workgroup is past its wait
-            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned d = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == (unsigned)S - 1) {  // every finisher is past its wait
+            __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
