@@ -244,6 +244,17 @@ int llmi_context_attention_qkv(const float* qkv, const int32_t* padding_offset, 
                                int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
                                int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
                                llmi_stream_t stream);
+/* llmi_context_attention_qkv preceded by its q/k/v projection (context_attention.cpp:99's
+ * launchLinearGemm): qkv = x [num_tokens, hidden] . w_qkv^T ((heads + 2 kv_heads) * head_dim
+ * rows, fp16) with llmi_linear's arithmetic, its K slices summed in slice order by the RoPE
+ * kernel as it reads them (the same values, no [num_tokens, qkv] pass). LLMI_EUNSUPPORTED
+ * (nothing launched) for other weight dtypes / shapes: the caller runs llmi_linear first. */
+int llmi_context_attention_proj(const float* x, const void* w_qkv, int w_dtype, int hidden,
+                                const int32_t* padding_offset, const int32_t* history_length,
+                                const int32_t* input_length, int num_tokens, int batch, int max_q_len, int heads,
+                                int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
+                                int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
+                                llmi_stream_t stream);
 
 /* launchScaleMaskAndSoftmax (src/kernels/attn_softmax_kernel.h:8-12, .cu:79-174):
  * score[b, h, q, :] = softmax(scale * qk[b, h, q, :] + (1 - mask[b, q, :]) * -10000)

@@ -560,7 +560,8 @@ public:
     }
 
     // forward's steps 1-5 without o_proj, fused core only (fused(), after allocForForward):
-    // qkv projection of x (fp32 [num_tokens, H]), then RoPE with the k / v rows stored
+    // qkv projection of x (fp32 [num_tokens, H]; for fp16 weights inside
+    // llmi_context_attention_proj, its K slices summed by the RoPE kernel), then RoPE with the k / v rows stored
     // straight into the cache after the history, then the attention core over the cache (one
     // launch each; fp16 caches are read as they are: the unfused chain widens exactly these
     // values to fp32). Returns the [num_tokens, H] attention rows, valid until freeBuf().
@@ -569,18 +570,31 @@ public:
                                       LLaMAAttentionStaticParams& static_params) {
         LLM_CHECK_WITH_INFO(fused() && qkv_buf_wo_pad_1, "forwardCore: fused core after allocForForward only");
         const DataType cdt = outputs["all_k_cache"]->dtype;
-        cublasWrapper cw{stream};
-        launchLinearGemm(x, weights.qkv, qkv_buf_wo_pad, cublas_wrapper ? cublas_wrapper : &cw, false, true);
         void* kcache = cdt == FP32 ? (void*)outputs["all_k_cache"]->as<float>()->data
                                    : (void*)outputs["all_k_cache"]->as<half_t>()->data;
         void* vcache = cdt == FP32 ? (void*)outputs["all_v_cache"]->as<float>()->data
                                    : (void*)outputs["all_v_cache"]->as<half_t>()->data;
-        LLMI_CALL(llmi_context_attention_qkv(
-            qkv_buf_wo_pad->data, inputs["padding_offset"]->as<int>()->data, inputs["history_length"]->as<int>()->data,
-            inputs["input_length"]->as<int>()->data, params.num_tokens, params.batch_size, params.max_q_len, head_num,
-            kv_head_num, head_size, static_params.rotary_embedding_base, kcache, vcache,
-            cdt == FP32 ? LLMI_F32 : LLMI_F16, inputs["layer_id"]->as<int>()->getVal(),
-            outputs["all_k_cache"]->shape[3], scale, q_buf_w_pad->data, qkv_buf_wo_pad_1->data, stream));
+        const int* po = inputs["padding_offset"]->as<int>()->data;
+        const int* hist = inputs["history_length"]->as<int>()->data;
+        const int* ql = inputs["input_length"]->as<int>()->data;
+        const int cd = cdt == FP32 ? LLMI_F32 : LLMI_F16, layer = inputs["layer_id"]->as<int>()->getVal();
+        const int max_seq = outputs["all_k_cache"]->shape[3];
+        const float base = static_params.rotary_embedding_base;
+        // fp16 weights: the projection's K slices go straight into the RoPE kernel
+        int rc = llmi_context_attention_proj(x->data, weights.qkv.data, llmiWeightDtype(getWeightType<T>()),
+                                             weights.qkv.shape[1], po, hist, ql, params.num_tokens, params.batch_size,
+                                             params.max_q_len, head_num, kv_head_num, head_size, base, kcache, vcache,
+                                             cd, layer, max_seq, scale, q_buf_w_pad->data, qkv_buf_wo_pad_1->data,
+                                             stream);
+        if (rc == LLMI_EUNSUPPORTED) {
+            cublasWrapper cw{stream};
+            launchLinearGemm(x, weights.qkv, qkv_buf_wo_pad, cublas_wrapper ? cublas_wrapper : &cw, false, true);
+            rc = llmi_context_attention_qkv(qkv_buf_wo_pad->data, po, hist, ql, params.num_tokens, params.batch_size,
+                                            params.max_q_len, head_num, kv_head_num, head_size, base, kcache, vcache,
+                                            cd, layer, max_seq, scale, q_buf_w_pad->data, qkv_buf_wo_pad_1->data,
+                                            stream);
+        }
+        LLMI_CALL(rc);
         return qkv_buf_wo_pad_1;
     }
 

@@ -249,6 +249,30 @@ int llmi_context_attention_qkv(const float* qkv, const int32_t* padding_offset, 
                                         layer, max_seq, scale, q_scratch, out, STREAM(stream));
 }
 
+int llmi_context_attention_proj(const float* x, const void* w_qkv, int w_dtype, int hidden,
+                                const int32_t* padding_offset, const int32_t* history_length,
+                                const int32_t* input_length, int num_tokens, int batch, int max_q_len, int heads,
+                                int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
+                                int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
+                                llmi_stream_t stream) {
+    LLMI_REQUIRE(x && w_qkv && num_tokens >= 1 && hidden >= 1 && heads >= 1 && kv_heads >= 1 && head_dim >= 1,
+                 "context_attention_proj: bad arguments");
+    const int n = (heads + 2 * kv_heads) * head_dim;
+    if (w_dtype != LLMI_F16 || !linear_mfma_supported(num_tokens, n, hidden) ||
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w_qkv)) & 15)) {
+        set_last_error("[llmi][ERROR] context_attention_proj: needs fp16 weights, >= 16 rows, GEMM-tileable "
+                       "shapes and 16-B aligned x / w (use llmi_linear + llmi_context_attention_qkv)");
+        return LLMI_EUNSUPPORTED;
+    }
+    const float* slab = nullptr;
+    int ks = 0;
+    LLMI_TRY(linear_mfma_launch(x, w_qkv, nullptr, num_tokens, n, hidden, STREAM(stream), nullptr, &slab, &ks));
+    return context_attention_qkv_launch(slab, padding_offset, history_length, input_length, num_tokens, batch,
+                                        max_q_len, heads, kv_heads, head_dim, rope_base, k_cache, v_cache, cache_dtype,
+                                        layer, max_seq, scale, q_scratch, out, STREAM(stream), ks,
+                                        (size_t)num_tokens * n);
+}
+
 int llmi_causal_mask(void* mask, int dtype, const int32_t* q_lens, const int32_t* k_lens, int batch,
                      int max_q_len, int max_k_len, llmi_stream_t stream) {
     return causal_mask_launch(mask, dtype, q_lens, k_lens, batch, max_q_len, max_k_len, STREAM(stream));

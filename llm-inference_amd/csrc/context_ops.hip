@@ -115,12 +115,19 @@ __device__ __forceinline__ void rope_angle(int pos, int i, int d, float base, fl
 }
 
 // the rotated pair (x0 c - x1 s, x1 c + x0 s) with every product and sum rounded on its own
-// (no fma contraction), so the launcher and the fused-to-cache form below give the same bits
+// (no fma contraction), so the launcher and the fused-to-cache form below give the same bits.
+// The empty asm pins each product in a register: __fmul_rn / __fsub_rn alone still let
+// hipcc's fp-contract fold one product into the add, and which one depended on the
+// surrounding code (the per-token kernel's float4 form contracted rot_hi differently).
 __device__ __forceinline__ float rot_lo(float x0, float x1, float c, float s) {
-    return __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
+    float a = x0 * c, b = x1 * s;
+    asm volatile("" : "+v"(a), "+v"(b));
+    return a - b;
 }
 __device__ __forceinline__ float rot_hi(float x0, float x1, float c, float s) {
-    return __fadd_rn(__fmul_rn(x1, c), __fmul_rn(x0, s));
+    float a = x1 * c, b = x0 * s;
+    asm volatile("" : "+v"(a), "+v"(b));
+    return a + b;
 }
 
 // add_fusedQKV_bias_transpose_kernel (qkv_bias_and_RoPE.cu:49-144), Llama (no bias):
@@ -154,36 +161,76 @@ __global__ void rope_qkv_prefill_kernel(const T* qkv, T* q_buf, T* k_buf, T* v_b
 // The same rotation with the new k / v rows stored straight into the layer's cache at
 // slot history[b] + s (launchConcatKVCache's placement, concat_past_kv.cu:122), rounded
 // to KT on the store -- what the separate append stores -- so the padded k / v buffers
-// are never written. fp32 activations.
+// are never written. fp32 activations, d = 128, one workgroup per token: the token's 64
+// angles once into LDS (a form with a workgroup per (token, head) recomputed them for
+// every head, a double pow + sincos per pair: 17 us per 7B layer at 512 rows), then every
+// head's pairs as float4s, four pairs per lane step. qkv may arrive as ks > 1 K slices of
+// the projection ks_stride floats apart (llmi_context_attention_proj): they are summed in
+// slice order on the load, slab_sum_kernel's order, so the values are the same bits.
 template <typename KT>
-__global__ void rope_qkv_cache_kernel(const float* qkv, float* q_buf, KT* k_cache, KT* v_cache, const int* po,
-                                      const int* hist, int seq_len, int heads, int kv_heads, int d, float base,
-                                      int max_seq) {
-    const int tok = blockIdx.x, h = blockIdx.y, t = threadIdx.x;
+__global__ __launch_bounds__(256) void rope_qkv_cache_tok_kernel(const float* qkv, float* q_buf, KT* k_cache,
+                                                                 KT* v_cache, const int* po, const int* hist,
+                                                                 int seq_len, int heads, int kv_heads, float base,
+                                                                 int max_seq, int ks, size_t ks_stride) {
+    constexpr int d = 128, d4 = d / 8;  // float4 steps per half-row
+    __shared__ __attribute__((aligned(16))) float cs_s[d / 2], sn_s[d / 2];
+    const int tok = blockIdx.x, t = threadIdx.x;
     const int p = tok + po[tok], b = p / seq_len, s = p % seq_len;
+    const int pos = hist[b] + s;
+    if (t < d / 2) rope_angle(pos, t, d, base, &cs_s[t], &sn_s[t]);
+    __syncthreads();
     const float* row = qkv + (size_t)tok * (heads + 2 * kv_heads) * d;
-    const size_t qo = (((size_t)b * heads + h) * seq_len + s) * d;
-    const size_t co = (((size_t)b * kv_heads + h) * max_seq + hist[b] + s) * d;
-    if (t < d / 2) {
-        float c, sn;
-        rope_angle(hist[b] + s, t, d, base, &c, &sn);
-        const float* qh = row + (size_t)h * d;
-        const float q0 = qh[t], q1 = qh[t + d / 2];
-        q_buf[qo + t] = rot_lo(q0, q1, c, sn);
-        q_buf[qo + t + d / 2] = rot_hi(q0, q1, c, sn);
-        if (h < kv_heads) {
-            const float* kh = row + (size_t)(heads + h) * d;
-            const float k0 = kh[t], k1 = kh[t + d / 2];
-            float r0 = rot_lo(k0, k1, c, sn), r1 = rot_hi(k0, k1, c, sn);
-            // keep the fp32 result: with a half cache the compiler would otherwise fold the
-            // last product and the conversion into one v_fma_mix (a single rounding to fp16),
-            // while the launcher + append round twice (fp32, then fp16)
-            asm volatile("" : "+v"(r0), "+v"(r1));
-            stf(k_cache + co + t, r0);
-            stf(k_cache + co + t + d / 2, r1);
+    auto ld4 = [&](const float* src) {
+        float4 a = *reinterpret_cast<const float4*>(src);
+        for (int k = 1; k < ks; ++k) {
+            const float4 c = *reinterpret_cast<const float4*>(src + k * ks_stride);
+            a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
         }
+        return a;
+    };
+    auto rot4 = [&](const float* src, int j, float4& lo, float4& hi) {
+        const float4 x0 = ld4(src + 4 * j);
+        const float4 x1 = ld4(src + d / 2 + 4 * j);
+        const float4 c = *reinterpret_cast<const float4*>(cs_s + 4 * j);
+        const float4 sn = *reinterpret_cast<const float4*>(sn_s + 4 * j);
+        lo = make_float4(rot_lo(x0.x, x1.x, c.x, sn.x), rot_lo(x0.y, x1.y, c.y, sn.y), rot_lo(x0.z, x1.z, c.z, sn.z),
+                         rot_lo(x0.w, x1.w, c.w, sn.w));
+        hi = make_float4(rot_hi(x0.x, x1.x, c.x, sn.x), rot_hi(x0.y, x1.y, c.y, sn.y), rot_hi(x0.z, x1.z, c.z, sn.z),
+                         rot_hi(x0.w, x1.w, c.w, sn.w));
+    };
+    for (int e = t; e < heads * d4; e += 256) {  // q heads
+        const int h = e / d4, j = e % d4;
+        float4 lo, hi;
+        rot4(row + (size_t)h * d, j, lo, hi);
+        float* qo = q_buf + (((size_t)b * heads + h) * seq_len + s) * d;
+        *reinterpret_cast<float4*>(qo + 4 * j) = lo;
+        *reinterpret_cast<float4*>(qo + d / 2 + 4 * j) = hi;
     }
-    if (h < kv_heads && t < d) stf(v_cache + co + t, row[(size_t)(heads + kv_heads + h) * d + t]);
+    auto st4 = [](KT* dst, float4 v) {
+        if constexpr (std::is_same<KT, float>::value) {
+            *reinterpret_cast<float4*>(dst) = v;
+        } else {
+            dst[0] = __float2half(v.x); dst[1] = __float2half(v.y); dst[2] = __float2half(v.z); dst[3] = __float2half(v.w);
+        }
+    };
+    for (int e = t; e < kv_heads * d4; e += 256) {  // k heads into the cache slot
+        const int h = e / d4, j = e % d4;
+        float4 lo, hi;
+        rot4(row + (size_t)(heads + h) * d, j, lo, hi);
+        // keep the fp32 results: with a half cache the compiler would otherwise fold the last
+        // product and the conversion into one v_fma_mix (a single rounding to fp16), while
+        // the launcher + append round twice (fp32, then fp16)
+        asm volatile("" : "+v"(lo.x), "+v"(lo.y), "+v"(lo.z), "+v"(lo.w));
+        asm volatile("" : "+v"(hi.x), "+v"(hi.y), "+v"(hi.z), "+v"(hi.w));
+        KT* ko = k_cache + (((size_t)b * kv_heads + h) * max_seq + pos) * d;
+        st4(ko + 4 * j, lo);
+        st4(ko + d / 2 + 4 * j, hi);
+    }
+    for (int e = t; e < kv_heads * (d / 4); e += 256) {  // v heads
+        const int h = e / (d / 4), j = e % (d / 4);
+        const float4 v = ld4(row + (size_t)(heads + kv_heads + h) * d + 4 * j);
+        st4(v_cache + (((size_t)b * kv_heads + h) * max_seq + pos) * d + 4 * j, v);
+    }
 }
 
 bool fp_dtype(int dt) { return dt == LLMI_F32 || dt == LLMI_F16; }
@@ -408,6 +455,191 @@ __global__ __launch_bounds__(kCThreads) void ctx_attn_kernel(const float* q, con
                 make_float4(o[4 * r] * inv, o[4 * r + 1] * inv, o[4 * r + 2] * inv, o[4 * r + 3] * inv);
     }
 }
+
+// The same attention on the f32-input matrix cores (v_mfma_f32_16x16x4_f32: exact fp32,
+// each instruction a k-ordered fmaf chain, at 64 FLOP/clk/SIMD -- the fp32 VALU peak,
+// without the VALU kernel's LDS operand traffic per FMA). Block: 16 queries, 4 waves that
+// split the block's 32-key chunks (wave w takes chunks w, w + 4, ...: a wave's dependent
+// MFMA chain is the kernel's critical path at 32 cycles per instruction, so the keys, not
+// the queries, are spread over the SIMDs), each wave's K / V rows straight from the cache
+// into registers (L2 serves the other query blocks of the sequence), then the four
+// (m, l, O) partials merged through LDS. Every product is computed transposed so that one
+// query stays in one lane column (lane & 15) throughout:
+//   S^T[key][query] = K . Q^T:  A = K rows (lane: key lane & 15, d 32 g + s, g = lane >> 4),
+//                               B = Q (lane: query lane & 15, the same d) held in 32 VGPRs;
+//                               result lane: keys 4 g + q (q < 4) of the tile, query lane & 15
+//   O^T[d][query] += V^T . P^T: A = V^T (lane: d = 8 (lane & 15) + j for O tile j, key
+//                               16 t + 4 g + s), B = the lane's own p of that key;
+//                               result lane: d = 8 (4 g + q) + j, query lane & 15
+// so the online-softmax max / sum over a chunk's keys is 8 registers then 2 cross-group
+// shuffles, and the rescale by alpha needs no data movement. Roofline: MFMA f32
+// (157 TFLOP/s); FLOPs 4 x d x the visible (query, key) pairs.
+#ifndef LLMI_CTXA_EXP
+#define LLMI_CTXA_EXP 0
+#endif
+constexpr int kMQ = 16, kMKC = 32, kMW = 4;
+template <typename KT> __device__ __forceinline__ void ld8f(const KT* p, float* v) {
+    if constexpr (std::is_same<KT, float>::value) {
+        const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+        const uint4 u = *reinterpret_cast<const uint4*>(p);
+        const __half2* h = reinterpret_cast<const __half2*>(&u);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float2 f = __half22float2(h[i]);
+            v[2 * i] = f.x;
+            v[2 * i + 1] = f.y;
+        }
+    }
+}
+template <typename KT>
+__global__ __launch_bounds__(256, 2) void ctx_attn_mfma_kernel(const float* q, const KT* k_cache, const KT* v_cache,
+                                                               const int* hist, const int* qlen, int batch, int heads,
+                                                               int kv_heads, int max_q, int max_seq, float scale,
+                                                               float* out) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) float o_s[kMW * kMQ * kCLd];
+    __shared__ float ml_s[kMW][2][kMQ];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, g = lane >> 4, c = lane & 15;
+    // XCD-aware order (1-D grid, workgroup id % 8 = its XCD): every query block of one
+    // (sequence, head) pair runs on the same XCD, so that XCD's 4-MB L2 holds the pair's K / V
+    // for all of them (with the blocks spread over the XCDs each L2 saw every pair's K / V,
+    // 17 MB at 7B width, and the re-reads went to HBM); longest query blocks first
+    const int nqb = (max_q + kMQ - 1) / kMQ, pairs = heads * batch;
+    const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;
+    const int per = (pairs - xcd + 7) / 8;  // pairs xcd, xcd + 8, ... live on this XCD
+    if (r >= per * nqb) return;
+    const int pair = xcd + 8 * (r % per);
+    const int b = pair / heads, h = pair % heads;
+    const int ql = qlen[b], h0 = hist[b];
+    const int q_first = (nqb - 1 - r / per) * kMQ;
+    if (q_first >= ql) return;  // uniform: a padded block
+    int tok0 = 0;
+    for (int i = 0; i < b; ++i) tok0 += qlen[i];
+    const int kvh = h / (heads / kv_heads);
+    const int q_row = min(q_first + c, ql - 1);  // rows past the sequence compute, never store
+    const int my_pos = h0 + q_row;
+    const int kend = h0 + min(q_first + kMQ, ql);  // the block's keys [0, kend)
+    float qr[32];
+    {
+        const float* qp = q + (((size_t)b * heads + h) * max_q + q_row) * kCD + 32 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ld8f(qp + 8 * i, qr + 8 * i);
+    }
+    const KT* kc = k_cache + ((size_t)b * kv_heads + kvh) * max_seq * kCD;
+    const KT* vc = v_cache + ((size_t)b * kv_heads + kvh) * max_seq * kCD;
+    float m_run = -INFINITY, l_run = 0.f;
+    f4v o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int nch = (kend + kMKC - 1) / kMKC;
+    for (int ch = w; ch < nch; ch += kMW) {  // wave-uniform
+        const int k0 = ch * kMKC;
+        // this chunk's K rows (key 16 tt + c, dims 32 g ..) and V rows (key 16 tt + 4 g + ss,
+        // dims 8 c ..), keys past the block clamped (masked below)
+        float ka[2][32], va[2][4][8];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const KT* kp = kc + (size_t)min(k0 + 16 * tt + c, kend - 1) * kCD + 32 * g;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ld8f(kp + 8 * i, ka[tt] + 8 * i);
+        }
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int ss = 0; ss < 4; ++ss)
+                ld8f(vc + (size_t)min(k0 + 16 * tt + 4 * g + ss, kend - 1) * kCD + 8 * c, va[tt][ss]);
+        f4v s0 = f4v{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+#if LLMI_CTXA_EXP == 1  // timing only: S by VALU sums (loads kept, MFMAs gone)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            s0[i & 3] += ka[0][i] * qr[i];
+            s1[i & 3] += ka[1][i] * qr[i];
+        }
+#else
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[0][i], qr[i], s0, 0, 0, 0);
+            s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[1][i], qr[i], s1, 0, 0, 0);
+        }
+#endif
+        // mask + scale (the reference's scale * qk), chunk max and exp
+        float p[2][4];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const int j0 = k0 + 4 * g + qq, j1 = j0 + 16;
+            p[0][qq] = (j0 > my_pos || j0 >= kend) ? -INFINITY : scale * s0[qq];
+            p[1][qq] = (j1 > my_pos || j1 >= kend) ? -INFINITY : scale * s1[qq];
+            mx = fmaxf(mx, fmaxf(p[0][qq], p[1][qq]));
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        // a chunk wholly past this query's position leaves m at -inf and p = 0 (the wave's
+        // first chunk may be such a chunk: only wave 0 starts at key 0)
+        const float m_new = fmaxf(m_run, mx);
+        const float m_use = m_new == -INFINITY ? 0.f : m_new;
+        const float alpha = expf(m_run - m_use);
+        float ps = 0.f;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                p[tt][qq] = expf(p[tt][qq] - m_use);
+                ps += p[tt][qq];
+            }
+        ps += __shfl_xor(ps, 16);
+        ps += __shfl_xor(ps, 32);
+        l_run = l_run * alpha + ps;
+        m_run = m_new;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= alpha;
+        // O^T += V^T . P^T over the chunk's 32 keys, 4 per step (key 16 tt + 4 g + ss)
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+#if LLMI_CTXA_EXP == 2  // timing only: PV by VALU (loads kept, MFMAs gone)
+                    o[j][ss] += va[tt][ss][j] * p[tt][ss];
+#else
+                    o[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[tt][ss][j], p[tt][ss], o[j], 0, 0, 0);
+#endif
+    }
+    // merge the four waves' partials: M = max m_w, L = sum l_w e^(m_w - M), O likewise
+    if (g == 0) {
+        ml_s[w][0][c] = m_run;
+        ml_s[w][1][c] = l_run;
+    }
+    float* ow = o_s + (w * kMQ + c) * kCLd;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+        float4* dst = reinterpret_cast<float4*>(ow + 8 * (4 * g + qq));
+        dst[0] = make_float4(o[0][qq], o[1][qq], o[2][qq], o[3][qq]);
+        dst[1] = make_float4(o[4][qq], o[5][qq], o[6][qq], o[7][qq]);
+    }
+    __syncthreads();
+    const int qi = t >> 4, d0 = 8 * (t & 15);
+    if (q_first + qi >= ql) return;
+    float M = -INFINITY;
+#pragma unroll
+    for (int x = 0; x < kMW; ++x) M = fmaxf(M, ml_s[x][0][qi]);  // finite: wave 0 saw key 0
+    float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int x = 0; x < kMW; ++x) {
+        const float e = expf(ml_s[x][0][qi] - M);  // 0 for a wave that saw no visible key
+        L += ml_s[x][1][qi] * e;
+        const float* src = o_s + (x * kMQ + qi) * kCLd + d0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += src[i] * e;
+    }
+    const float inv = 1.0f / (L + 1e-6f);  // attn_softmax_kernel.cu: exp(x - max) / (sum + 1e-6)
+    float4* orow = reinterpret_cast<float4*>(out + ((size_t)(tok0 + q_first + qi) * heads + h) * kCD + d0);
+    orow[0] = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+    orow[1] = make_float4(acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv);
+}
 }  // namespace
 
 int context_attention_launch(const float* q, const void* k_cache, const void* v_cache, int cache_dtype, int layer,
@@ -420,6 +652,23 @@ int context_attention_launch(const float* q, const void* k_cache, const void* v_
                  "context_attention: bad shape");
     LLMI_REQUIRE(fp_dtype(cache_dtype), "context_attention: cache dtype must be f32 or f16");
     const size_t off = (size_t)layer * batch * kv_heads * max_seq * kCD;  // concat_past_kv.cu:122
+#ifndef LLMI_CTX_ATTN_FMA  // the VALU form below: A/B builds only
+    LLMI_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(out) |
+                   reinterpret_cast<uintptr_t>(k_cache) | reinterpret_cast<uintptr_t>(v_cache)) & 15) == 0,
+                 "context_attention: q, out and the caches must be 16-B aligned");
+    const int pairs = heads * batch, nqb = (max_q + kMQ - 1) / kMQ;
+    const dim3 mgrid(8 * ((pairs + 7) / 8) * nqb);
+    if (cache_dtype == LLMI_F32)
+        hipLaunchKernelGGL(ctx_attn_mfma_kernel<float>, mgrid, dim3(256), 0, s, q, (const float*)k_cache + off,
+                           (const float*)v_cache + off, history_length, input_length, batch, heads, kv_heads, max_q,
+                           max_seq, scale, out);
+    else
+        hipLaunchKernelGGL(ctx_attn_mfma_kernel<__half>, mgrid, dim3(256), 0, s, q, (const __half*)k_cache + off,
+                           (const __half*)v_cache + off, history_length, input_length, batch, heads, kv_heads, max_q,
+                           max_seq, scale, out);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+#endif
     const dim3 grid((max_q + kCQB - 1) / kCQB, heads, batch);
     if (cache_dtype == LLMI_F32)
         hipLaunchKernelGGL(ctx_attn_kernel<float>, grid, dim3(kCThreads), 0, s, q, (const float*)k_cache + off,
@@ -437,22 +686,25 @@ int context_attention_qkv_launch(const float* qkv, const int* padding_offset, co
                                  const int* input_length, int num_tokens, int batch, int max_q, int heads,
                                  int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
                                  int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
-                                 hipStream_t s) {
+                                 hipStream_t s, int ks, size_t ks_stride) {
     LLMI_REQUIRE(qkv && padding_offset && k_cache && v_cache && q_scratch, "context_attention_qkv: null pointer");
+    LLMI_REQUIRE(ks >= 1 && (ks == 1 || ks_stride % 4 == 0), "context_attention_qkv: bad slice count / stride");
     LLMI_REQUIRE(num_tokens > 0 && num_tokens <= batch * max_q && head_dim == kCD && kv_heads > 0 &&
                      heads % kv_heads == 0 && heads <= 65535,
                  "context_attention_qkv: bad shape");
     LLMI_REQUIRE(fp_dtype(cache_dtype), "context_attention_qkv: cache dtype must be f32 or f16");
     const size_t off = (size_t)layer * batch * kv_heads * max_seq * kCD;
-    const dim3 grid(num_tokens, heads);
+    LLMI_REQUIRE(((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(q_scratch)) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(k_cache) & 7) == 0 && (reinterpret_cast<uintptr_t>(v_cache) & 7) == 0,
+                 "context_attention_qkv: qkv and q_scratch 16-B, the caches 8-B aligned");
     if (cache_dtype == LLMI_F32)
-        hipLaunchKernelGGL(rope_qkv_cache_kernel<float>, grid, dim3(kCD), 0, s, qkv, q_scratch,
+        hipLaunchKernelGGL(rope_qkv_cache_tok_kernel<float>, dim3(num_tokens), dim3(256), 0, s, qkv, q_scratch,
                            (float*)k_cache + off, (float*)v_cache + off, padding_offset, history_length, max_q,
-                           heads, kv_heads, kCD, rope_base, max_seq);
+                           heads, kv_heads, rope_base, max_seq, ks, ks_stride);
     else
-        hipLaunchKernelGGL(rope_qkv_cache_kernel<__half>, grid, dim3(kCD), 0, s, qkv, q_scratch,
+        hipLaunchKernelGGL(rope_qkv_cache_tok_kernel<__half>, dim3(num_tokens), dim3(256), 0, s, qkv, q_scratch,
                            (__half*)k_cache + off, (__half*)v_cache + off, padding_offset, history_length, max_q,
-                           heads, kv_heads, kCD, rope_base, max_seq);
+                           heads, kv_heads, rope_base, max_seq, ks, ks_stride);
     LLMI_HIP(hipGetLastError());
     return context_attention_launch(q_scratch, k_cache, v_cache, cache_dtype, layer, history_length, input_length,
                                     batch, heads, kv_heads, max_q, max_seq, head_dim, scale, out, s);

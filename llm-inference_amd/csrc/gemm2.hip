@@ -460,6 +460,8 @@ __global__ __launch_bounds__(kThreads) void resid_norm_kernel(float* resid, cons
     float4* rr = reinterpret_cast<float4*>(resid) + row * n4;
     float4 v[NPT];
     float ss = 0.f;
+    // (an instance with the 8 slices' loads all issued first measured 22.8 vs 20.1 us at
+    // 512 x 4096: the slice-at-a-time loop below keeps more rows in flight per CU)
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
         const int j = threadIdx.x + i * kThreads;
@@ -548,8 +550,8 @@ bool linear_mfma_supported(int m, int n, int k) {
 }
 
 int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s,
-                       const ResidEpi* re) {
-    LLMI_REQUIRE(x && w && (y || re) && linear_mfma_supported(m, n, k),
+                       const ResidEpi* re, const float** slab_out, int* ks_out) {
+    LLMI_REQUIRE(x && w && (y || re || (slab_out && ks_out)) && linear_mfma_supported(m, n, k),
                  "linear_mfma: N a multiple of 128, K of 64, M >= 16");
     LLMI_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
                  "linear_mfma: x and y must be 16-B aligned");
@@ -564,7 +566,8 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
         ks = nk;
     }
     const size_t plane = ((size_t)m * k * 2 + 255) / 256 * 256;
-    const size_t slab = ks > 1 || re ? (size_t)ks * m * n * 4 : 0;  // the residual form: always (>= 1) slices
+    const bool raw = slab_out != nullptr;  // the slices themselves, for a consumer that sums them
+    const size_t slab = ks > 1 || re || raw ? (size_t)ks * m * n * 4 : 0;  // residual / raw forms: >= 1 slice
     char* ws = nullptr;
     LLMI_TRY(linear_workspace(s, 2 * plane + slab, &ws));
     _Float16* hi = reinterpret_cast<_Float16*>(ws);
@@ -578,11 +581,16 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
     g.w = w; g.m = m; g.n = n; g.k = k; g.ldy = n;
     float* sl = reinterpret_cast<float*>(ws + 2 * plane);
     if (ks > 1) {
-        g.epi = EPI_SLAB; g.ksplit = ks; g.slab = sl; g.y = re ? sl : y;
+        g.epi = EPI_SLAB; g.ksplit = ks; g.slab = sl; g.y = re || raw ? sl : y;
     } else {
-        g.epi = EPI_STORE; g.y = re ? sl : y;
+        g.epi = EPI_STORE; g.y = re || raw ? sl : y;
     }
     LLMI_TRY(g3 ? gemm3_launch(g, s) : gemm2_launch(g, s));
+    if (raw) {
+        *slab_out = sl;
+        *ks_out = ks;
+        return LLMI_OK;
+    }
     if (re) return resid_norm_launch(*re, sl, ks, m, n, s);
     if (ks > 1) {
         const size_t n4y = (size_t)m * n / 4;

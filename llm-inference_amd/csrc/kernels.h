@@ -159,8 +159,10 @@ int gemm3_launch(Gemm2Args a, hipStream_t s);
 // llmi_linear for fp16 weights (the layer API's projections): fp32 x split into planes,
 // then gemm3 / gemm2 (+ split-K slices summed in order); see gemm2.hip
 bool linear_mfma_supported(int m, int n, int k);
+// slab_out / ks_out: the ks K slices ([ks][m][n] fp32 in the stream's linear workspace,
+// valid until the next llmi_linear-family call on s) instead of their sum
 int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, int k, hipStream_t s,
-                       const ResidEpi* re = nullptr);
+                       const ResidEpi* re = nullptr, const float** slab_out = nullptr, int* ks_out = nullptr);
 // rows of x (+= the ksplit slices of slab, in slice order, written back to x),
 // then optional RMSNorm, then fp16 planes hi[, lo] (hi null: the combine alone)
 int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_dtype, float eps, _Float16* hi,
@@ -359,7 +361,7 @@ int context_attention_qkv_launch(const float* qkv, const int* padding_offset, co
                                  const int* input_length, int num_tokens, int batch, int max_q, int heads,
                                  int kv_heads, int head_dim, float rope_base, void* k_cache, void* v_cache,
                                  int cache_dtype, int layer, int max_seq, float scale, float* q_scratch, float* out,
-                                 hipStream_t s);
+                                 hipStream_t s, int ks = 1, size_t ks_stride = 0);  // qkv as ks summed K slices
 int kv_append_launch(const void* k_src, const void* v_src, int dtype, int layer, const int* cur_q, const int* hist,
                      int batch, int kv_heads, int max_q, int d, int max_seq, void* k_cache, void* v_cache,
                      hipStream_t s);

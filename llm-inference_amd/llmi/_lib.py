@@ -60,6 +60,8 @@ _SIGS = {
     "llmi_context_attention": (_I, [_P, _P, _P, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P]),
     "llmi_context_attention_qkv": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _I, _I, _I, _F, _P,
                                         _P, _P]),
+    "llmi_context_attention_proj": (_I, [_P, _P, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P, _I, _I, _I,
+                                         _F, _P, _P, _P]),
     "llmi_ffn": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _P]),
     "llmi_linear_residual": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P]),
     "llmi_ffn_residual": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P]),

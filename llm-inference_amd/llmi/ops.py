@@ -258,6 +258,25 @@ def context_attention_qkv(qkv, padding_offset, history_length, input_length, bat
     return out
 
 
+def context_attention_proj(x, w_qkv, padding_offset, history_length, input_length, batch: int, max_q_len: int,
+                           heads: int, kv_heads: int, k_cache, v_cache, layer: int = 0, base: float = 10000.0,
+                           scale: float = None):
+    """context_attention_qkv with the q/k/v projection in front (llmi_context_attention_proj):
+    x [num_tokens, hidden] fp32, w_qkv [(heads + 2 kv) * 128, hidden] fp16. Raises LlmiError
+    (unsupported) where the fused form does not apply."""
+    _dev(x, w_qkv, padding_offset, history_length, input_length, k_cache, v_cache)
+    n, hidden, d = x.shape[0], x.shape[1], 128
+    po, hist, ql = _i32(padding_offset), _i32(history_length), _i32(input_length)
+    qs = torch.empty(batch, heads, max_q_len, d, device=x.device, dtype=torch.float32)
+    out = torch.empty(n, heads * d, device=x.device, dtype=torch.float32)
+    sc = 1.0 / math.sqrt(d) if scale is None else scale
+    call("llmi_context_attention_proj", x.contiguous().data_ptr(), w_qkv.data_ptr(), _dt(w_qkv), hidden,
+         po.data_ptr(), hist.data_ptr(), ql.data_ptr(), n, batch, max_q_len, heads, kv_heads, d, float(base),
+         k_cache.data_ptr(), v_cache.data_ptr(), _dt(k_cache), int(layer), k_cache.shape[3], float(sc), qs.data_ptr(),
+         out.data_ptr(), _stream())
+    return out
+
+
 def ffn(x, w_gate_up, w_down):
     """LLaMAFFNLayer for context rows in one call (llmi_ffn): x [m, hidden] fp32, w_gate_up
     [2 inter, hidden] and w_down [hidden, inter] fp16 -> [m, hidden] fp32. Raises

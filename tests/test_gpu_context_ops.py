@@ -261,6 +261,7 @@ def test_padding_offset_reference_example(ops):
     (4, 2, [5, 3, 7], [0, 4, 2]),          # GQA, ragged, history
     (8, 8, [33, 1, 64, 20], [31, 0, 3, 65]),  # chunks across 32-key blocks, one-token sequence
     (8, 1, [70], [0]),                     # MQA, one sequence past two query blocks
+    (8, 2, [130, 65, 17], [0, 40, 100]),   # past two 64-query blocks, partly filled waves
 ])
 def test_context_attention_qkv_fused_matches_oracle(ops, cache_dt, heads, kvh, lens, hist):
     """llmi_context_attention_qkv (RoPE + the k / v store into the cache + the ragged flash
@@ -388,3 +389,63 @@ def test_ffn_residual_matches_composition(ops, m):
     r64 = r0.astype(np.float64) + ((g / (1.0 + np.exp(-g))) * u) @ d64.T
     assert rel(N(r), r64) < 1e-5
     np.testing.assert_array_equal(N(xt), x)  # x read, never written (out is a new tensor here)
+
+
+@pytest.mark.parametrize("cache_dt", [np.float32, np.float16])
+def test_context_attention_fused_7b_ragged_timing(ops, cache_dt):
+    """The fused core at the context decoder's bench shape (Llama-2-7B heads, ragged lens
+    200 / 150 / 100 / 62, no history) against the oracle, timed with HIP events: the f32
+    MFMA kernel (context_ops.hip ctx_attn_mfma_kernel). Bar: the oracle's 1e-5 / 1e-4, and
+    40 us per layer -- the VALU form it replaced took ~43 us (r04n kernel stats)."""
+    rng = np.random.default_rng(21)
+    lens, hist, heads, d = [200, 150, 100, 62], [0, 0, 0, 0], 32, 128
+    n, batch, max_q = sum(lens), len(lens), max(lens)
+    qkv = rng.standard_normal((n, 3 * heads * d)).astype(np.float32)
+    kc = np.zeros((1, batch, heads, max_q, d), cache_dt)
+    vc = np.zeros((1, batch, heads, max_q, d), cache_dt)
+    want = C.context_attention(qkv, lens, np.array(hist), heads, heads, d, kc.copy(), vc.copy(), layer=0)
+    po = C.padding_offset(lens, max_q)
+    tdt = torch.float32 if cache_dt == np.float32 else torch.float16
+    tk, tv = T(kc, tdt), T(vc, tdt)
+    args = (T(qkv), T(po), T(np.array(hist, np.int32)), T(np.array(lens, np.int32)), batch, max_q, heads, heads, tk, tv)
+    got = N(ops.context_attention_qkv(*args, layer=0))
+    e = rel(got, want)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(20):
+        ops.context_attention_qkv(*args, layer=0)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 20 * 1e3
+    print(f"fused context attention 7B ragged {lens} cache {cache_dt.__name__}: rel-L2 {e:.2e}, {us:.1f} us "
+          f"(RoPE + cache store + attention)")
+    assert e < (1e-5 if cache_dt == np.float32 else 1e-4)
+    assert us < 60.0
+
+
+@pytest.mark.parametrize("cache_dt", [np.float32, np.float16])
+@pytest.mark.parametrize("lens,hist", [([200, 150, 100, 62], [0, 0, 0, 0]), ([40, 9, 33], [0, 7, 20])])
+def test_context_attention_proj_matches_linear_then_qkv(ops, cache_dt, lens, hist):
+    """llmi_context_attention_proj (the q/k/v projection's K slices summed by the RoPE kernel)
+    against llmi_linear followed by llmi_context_attention_qkv on the same inputs: the same
+    additions in the same order, so the attention output and the cache slots are bitwise equal
+    (7B-width heads at the bench's ragged shape: 2-slice split; fewer rows: other splits)."""
+    rng = np.random.default_rng(sum(lens))
+    heads, kvh, d, hidden = 32, 32, 128, 4096
+    n, batch, max_q = sum(lens), len(lens), max(lens)
+    max_seq = max(h + q for h, q in zip(hist, lens))
+    x = rng.standard_normal((n, hidden)).astype(np.float32)
+    w = (rng.standard_normal(((heads + 2 * kvh) * d, hidden)) / math.sqrt(hidden)).astype(np.float16)
+    kc = (rng.standard_normal((1, batch, kvh, max_seq, d)) * 0.5).astype(cache_dt)
+    vc = (rng.standard_normal((1, batch, kvh, max_seq, d)) * 0.5).astype(cache_dt)
+    po = C.padding_offset(lens, max_q)
+    tdt = torch.float32 if cache_dt == np.float32 else torch.float16
+    idx = (T(po), T(np.array(hist, np.int32)), T(np.array(lens, np.int32)), batch, max_q, heads, kvh)
+    k1, v1, k2, v2 = T(kc, tdt), T(vc, tdt), T(kc, tdt), T(vc, tdt)
+    got = N(ops.context_attention_proj(T(x), T(w), *idx, k1, v1))
+    qkv = ops.launchLinearGemm(T(x), T(w))
+    want = N(ops.context_attention_qkv(qkv, *idx, k2, v2))
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(N(k1), N(k2))
+    np.testing.assert_array_equal(N(v1), N(v2))
