@@ -493,6 +493,22 @@ template <typename KT> __device__ __forceinline__ void ld8f(const KT* p, float* 
         }
     }
 }
+// 8 values from raw 16-B vectors: two of fp32, one of fp16 (widened exactly)
+template <typename KT> __device__ __forceinline__ void unpack8(const uint4* r, float* v) {
+    if constexpr (std::is_same<KT, float>::value) {
+        const float* f = reinterpret_cast<const float*>(r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = f[i];
+    } else {
+        const __half2* h = reinterpret_cast<const __half2*>(r);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float2 f = __half22float2(h[i]);
+            v[2 * i] = f.x;
+            v[2 * i + 1] = f.y;
+        }
+    }
+}
 template <typename KT>
 __global__ __launch_bounds__(256, 2) void ctx_attn_mfma_kernel(const float* q, const KT* k_cache, const KT* v_cache,
                                                                const int* hist, const int* qlen, int batch, int heads,
@@ -537,19 +553,36 @@ __global__ __launch_bounds__(256, 2) void ctx_attn_mfma_kernel(const float* q, c
     for (int ch = w; ch < nch; ch += kMW) {  // wave-uniform
         const int k0 = ch * kMKC;
         // this chunk's K rows (key 16 tt + c, dims 32 g ..) and V rows (key 16 tt + 4 g + ss,
-        // dims 8 c ..), keys past the block clamped (masked below)
-        float ka[2][32], va[2][4][8];
+        // dims 8 c ..) as raw 16-B vectors, keys past the block clamped (masked below); all 32
+        // (fp32) / 16 (fp16) loads are issued before anything waits on one: left alone, the
+        // scheduler sank each load to its first use and waited there (~16 L2 round trips a
+        // chunk, 30 us per 7B layer at 512 ragged rows)
+        constexpr int R = std::is_same<KT, float>::value ? 2 : 1;  // 16-B vectors per 8 values
+        uint4 kraw[2][4 * R], vraw[2][4][R];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
-            const KT* kp = kc + (size_t)min(k0 + 16 * tt + c, kend - 1) * kCD + 32 * g;
+            const uint4* kp = reinterpret_cast<const uint4*>(kc + (size_t)min(k0 + 16 * tt + c, kend - 1) * kCD + 32 * g);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) ld8f(kp + 8 * i, ka[tt] + 8 * i);
+            for (int i = 0; i < 4 * R; ++i) kraw[tt][i] = kp[i];
         }
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-            for (int ss = 0; ss < 4; ++ss)
-                ld8f(vc + (size_t)min(k0 + 16 * tt + 4 * g + ss, kend - 1) * kCD + 8 * c, va[tt][ss]);
+            for (int ss = 0; ss < 4; ++ss) {
+                const uint4* vp =
+                    reinterpret_cast<const uint4*>(vc + (size_t)min(k0 + 16 * tt + 4 * g + ss, kend - 1) * kCD + 8 * c);
+#pragma unroll
+                for (int i = 0; i < R; ++i) vraw[tt][ss][i] = vp[i];
+            }
+        __builtin_amdgcn_sched_barrier(0);
+        float ka[2][32], va[2][4][8];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) unpack8<KT>(&kraw[tt][i * R], ka[tt] + 8 * i);
+#pragma unroll
+            for (int ss = 0; ss < 4; ++ss) unpack8<KT>(vraw[tt][ss], va[tt][ss]);
+        }
         f4v s0 = f4v{0.f, 0.f, 0.f, 0.f}, s1 = s0;
 #if LLMI_CTXA_EXP == 1  // timing only: S by VALU sums (loads kept, MFMAs gone)
 #pragma unroll
