@@ -18,6 +18,8 @@
 // around it dominate prefill (gemm.hip).
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace llmi {
@@ -258,8 +260,17 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
     char* Pw = Vt + D * KB * 2 + w * P * 16 * KB * 2;  // this wave's [P][16][128 B], chunk ^= row & 7
 
     const int nqb = (m_rows + QM - 1) / QM;
+    // XCD-aware 1-D grid (workgroup id % 8 = its XCD): every (query block, chunk) of one head
+    // runs on the same XCD, so that XCD's L2 holds the head's K / V for all of them (spread
+    // over the XCDs, each L2 saw every head's K / V, 8 MB at 7B width and 512 rows)
+    const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;
+    const int per = (heads - xcd + 7) / 8;  // heads xcd, xcd + 8, ... live on this XCD
+    int items = 0;  // (query block, chunk) items per head
+    for (int q = 0; q < nqb; ++q) items += (pf_nkb(q, p0, m_rows) + cb - 1) / cb;
+    if (r >= per * items) return;
+    const int h = xcd + 8 * (r % per);
     int qb = nqb - 1, chunk = 0, nch = 1;
-    for (int idx = blockIdx.x; qb >= 0; --qb) {  // longest (latest) query blocks first
+    for (int idx = r / per; qb >= 0; --qb) {  // longest (latest) query blocks first
         nch = (pf_nkb(qb, p0, m_rows) + cb - 1) / cb;
         if (idx < nch) {
             chunk = idx;
@@ -267,7 +278,6 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
         }
         idx -= nch;
     }
-    const int h = blockIdx.y;
     const int kvh = h / (heads / kv_heads);
     const int q_first = qb * QM;
     const float qscale = 1.0f / sqrtf((float)D);
@@ -614,6 +624,11 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
             }
             // (189-214 VGPRs: two workgroups per CU, so ~512 workgroups run in one round)
             int cb = a.split_ws ? std::max(2, (blocks * a.heads + 511) / 512) : max_nkb;
+            static const int cb_env = [] {  // tuning knob: key blocks per chunk (LLMI_PF_CHUNK)
+                const char* e = std::getenv("LLMI_PF_CHUNK");
+                return e ? std::atoi(e) : 0;
+            }();
+            if (a.split_ws && cb_env > 0) cb = cb_env;
             int maxc = (max_nkb + cb - 1) / cb;
             if (a.split_ws && (maxc > 8 || (size_t)a.heads * nqb * maxc * kPartFloats > a.split_ws_floats)) {
                 cb = max_nkb;  // no room: one chunk per query block
@@ -621,7 +636,8 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
             }
             int grid = 0;
             for (int qb = 0; qb < nqb; ++qb) grid += (pf_nkb(qb, a.p0, a.m) + cb - 1) / cb;
-            const dim3 gm(grid, a.heads);
+            // 1-D, XCD-interleaved: 8 x ceil(heads / 8) x (items per head) workgroups
+            const dim3 gm(8 * ((a.heads + 7) / 8) * grid);
             if (a.mfma_planes == 2)
                 hipLaunchKernelGGL(attn_prefill_mfma_kernel<2>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
                                    a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
