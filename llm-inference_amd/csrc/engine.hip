@@ -40,6 +40,8 @@
 #include <memory>
 #include <vector>
 
+#include <string>
+
 #include "kernels.h"
 #include "xchg_impl.h"
 #include "prng.h"
@@ -1089,16 +1091,28 @@ struct Engine {
         // (o slices into x) + rmsnorm + gate_up + silu * up -> planes of the down GEMM's input
         LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.ffn_norm, edt, c.rms_eps, pf_ah, lo, H, stream, pf_slab, so, f8));
         g.lda = H; g.w = L.gu; g.n = 2 * il; g.k = H;
+        static const bool sk_f8 = [] {  // fp8-lo gate_up: stream-K instead of the lo-pass balance
+            const char* e = std::getenv("LLMI_SK_F8");
+            return e && std::string(e) == "1";
+        }();
         if (f8) {  // + the fp8 lo pass spread over the CUs its 256 x 256 tiles leave idle (the
                    // fp16 lo pass balanced the same way measured 231 vs 225 us: not used)
             g.w8 = W8->gu; g.w8_exp = W8->gu_e;
-            g.bal_slab = pf_bal; g.bal_flags = pf_bal_flags; g.bal_grid = n_cu; g.err = &st->error;
+            if (!sk_f8) { g.bal_slab = pf_bal; g.bal_flags = pf_bal_flags; g.bal_grid = n_cu; }
+            g.err = &st->error;
         }
         g.epi = EPI_SILU_MUL; g.pair_off = il; g.y = nullptr; g.y_hi = pf_act_h(); g.y_lo = split >= 2 ? pf_act_l() : nullptr;
         g.ldy = il;
+        g.sk_slab = nullptr; g.sk_flags = nullptr; g.sk_grid = 0;
+        // the whole K work of gate_up's 172 tiles spread evenly over every CU (gemm3 stream-K)
+        if (gemm3_supported(g.n, H, EPI_SILU_MUL, 1) && (!f8 || sk_f8)) {
+            g.err = &st->error;
+            (void)gemm3_sk_attach(g, stream);
+        }
         LLMI_TRY(gemm3_supported(g.n, H, EPI_SILU_MUL, 1) ? gemm3_launch(g, stream) : gemm2_launch(g, stream));
         // down + residual: K slices into slabs (gemm3: 8 uneven slices, 256 workgroups)
         g.bal_slab = nullptr; g.bal_flags = nullptr;
+        g.sk_slab = nullptr; g.sk_flags = nullptr; g.sk_grid = 0;
         g.a[0] = pf_act_h(); g.a[1] = split >= 2 ? pf_act_l() : nullptr;
         g.lda = il; g.w = L.down; g.n = H; g.k = il;
         if (f8) { g.w8 = W8->down; g.w8_exp = W8->down_e; }

@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <string>
 #include <utility>
 
 #include "kernels.h"
@@ -543,7 +544,61 @@ int linear_workspace(hipStream_t s, size_t bytes, char** out) {
     return LLMI_OK;
 }
 int grid_of(size_t n4) { return (int)std::min<size_t>((n4 + kThreads - 1) / kThreads, 4096); }
+// gemm3 stream-K state per (device, stream): partial slots and their flags (zeroed when
+// allocated; every launch leaves them zero), grown like the linear workspace
+std::map<std::pair<int, hipStream_t>, std::pair<std::pair<void*, size_t>, std::pair<unsigned*, size_t>>> g_sk;
+int sk_workspace(hipStream_t s, size_t slab_bytes, size_t flag_bytes, float** slab, unsigned** flags) {
+    int dev = 0;
+    LLMI_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    auto& e = g_sk[{dev, s}];
+    if (slab_bytes > e.first.second || flag_bytes > e.second.second) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        LLMI_HIP(hipStreamIsCapturing(s, &cap));
+        LLMI_REQUIRE(cap == hipStreamCaptureStatusNone,
+                     "gemm3 stream-K: the workspace must grow, which cannot happen while the stream is capturing "
+                     "(run the same shapes once before capture)");
+        LLMI_HIP(hipStreamSynchronize(s));
+        const size_t sb = std::max(slab_bytes, e.first.second), fb = std::max(std::max(flag_bytes, e.second.second), (size_t)4);
+        if (e.first.first) LLMI_HIP(hipFree(e.first.first));
+        if (e.second.first) LLMI_HIP(hipFree(e.second.first));
+        e = {{nullptr, 0}, {nullptr, 0}};
+        LLMI_HIP(hipMalloc(&e.first.first, sb));
+        LLMI_HIP(hipMalloc(reinterpret_cast<void**>(&e.second.first), fb));
+        LLMI_HIP(hipMemset(e.second.first, 0, fb));
+        e.first.second = sb;
+        e.second.second = fb;
+    }
+    *slab = static_cast<float*>(e.first.first);
+    *flags = e.second.first;
+    return LLMI_OK;
+}
+int cu_count() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return n;
+}
+// stream-K for a gemm3 launch of these shapes when it keeps at most 3 partial slots per tile
+// (q/k/v and gate_up at 512 rows; o_proj / down, whose tiles would split 8 ways, keep the
+// split-K slices summed by their consumer). LLMI_SK=0 turns it off.
+bool sk_setup(Gemm2Args& g, hipStream_t s) {
+    static const bool off = [] {
+        const char* e = std::getenv("LLMI_SK");
+        return e && std::string(e) == "0";
+    }();
+    if (off) return false;
+    const int n_cu = cu_count();
+    const Gemm3SkPlan p = gemm3_sk_plan(g.m, g.n, g.k, g.epi, g.planes, g.lo8, n_cu);
+    if (p.pmax < 1 || p.pmax > 3) return false;
+    if (sk_workspace(s, p.slab_bytes, p.flag_bytes, &g.sk_slab, &g.sk_flags) != LLMI_OK) return false;
+    g.sk_grid = n_cu;
+    return true;
+}
 }  // namespace
+
+bool gemm3_sk_attach(Gemm2Args& g, hipStream_t s) { return sk_setup(g, s); }
 
 bool linear_mfma_supported(int m, int n, int k) {
     return m >= 16 && k % 64 == 0 && gemm2_supported(n, k, EPI_STORE);
@@ -559,6 +614,8 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
                                       "residual / out and an fp16 or fp32 gamma");
     const bool g3 = m >= 256 && gemm3_supported(n, k, EPI_STORE, 1);
     const int tiles = g3 ? ((m + 255) / 256) * (n / 256) : ((m + 127) / 128) * (n / kBN);
+    // (stream-K measured slower here than the 2-slice split: q/k/v 112 vs ~108 us with the
+    // slices' sum, its 256-KB partial slots being on the critical path; gate_up gains)
     int ks = 1;  // K slices while the tiles leave more than a third of the 256 CUs idle
     while (tiles * ks < 160 && ks < 8) {
         const int nk = ks * 2;
@@ -646,6 +703,7 @@ int ffn_mfma_launch(const float* x, const void* w_gu, const void* w_down, float*
     g.a[0] = xh; g.a[1] = xl; g.planes = 2; g.lda = hidden;
     g.w = w_gu; g.m = m; g.n = 2 * inter; g.k = hidden;
     g.epi = EPI_SILU_MUL; g.pair_off = inter; g.y = nullptr; g.y_hi = ah; g.y_lo = al; g.ldy = inter;
+    if (g3gu) sk_setup(g, s);  // stream-K when its tiles leave CUs idle
     LLMI_TRY(g3gu ? gemm3_launch(g, s) : gemm2_launch(g, s));
     Gemm2Args d;
     d.a[0] = ah; d.a[1] = al; d.planes = 2; d.lda = inter;

@@ -63,6 +63,7 @@ typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
 
 constexpr int kT = 512;              // 8 waves: (wr, wc) = (w >> 2, w & 3)
@@ -511,6 +512,131 @@ __global__ __launch_bounds__(kT) void gemm3_silu_bal_kernel(Gemm2Args a) {
     g3_epilogue<EPI_SILU_MUL>(a, lds, acc, m0, ct, 0);
 }
 
+// Stream-K: with fewer 256 x 256 tiles than CUs (gate_up's 172 and q/k/v's 96 at 512 rows
+// left 84 / 160 CUs idle for a whole launch) the tiles' K work -- per tile nh + nl virtual K
+// tiles ([hi | lo], taken in pairs: g3_run needs >= 2) -- is cut into sk_grid equal
+// contiguous ranges, one per workgroup, that cross tile boundaries. The workgroup holding a
+// tile's first pair owns it: that is the END of its range, so the tile's later pieces (the
+// START of the next workgroups' ranges) were computed first and the owner's wait is short.
+// Later pieces go to fp32 partial slots and set a flag; the owner waits for the flags
+// (bounded: error bit 16), resets them (a graph replay finds them zero), adds the slots in
+// order onto its own piece (repeatable sums) and runs the tile's epilogue. Every workgroup
+// is resident (sk_grid <= the CU count, one 136-KB workgroup per CU), so waits always end.
+struct SkDims {
+    int m_tiles, T, NH, U2;
+    long TP;
+};
+__host__ __device__ inline SkDims sk_dims(int m, int n_tiles, int k, int planes, int lo8) {
+    SkDims d;
+    d.m_tiles = (m + kTile - 1) / kTile;
+    d.T = d.m_tiles * n_tiles;
+    d.NH = k / kK;
+    const int NL = planes == 2 ? (lo8 ? k / (2 * kK) : k / kK) : 0;
+    d.U2 = (d.NH + NL) / 2;
+    d.TP = (long)d.T * d.U2;
+    return d;
+}
+__host__ __device__ inline int sk_wg_of(long x, long TP, int G) { return (int)(((x + 1) * G - 1) / TP); }
+
+template <int EPI>
+__global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int t = threadIdx.x;
+    const SkDims d = sk_dims(a.m, a.n_tiles, a.k, a.planes, a.lo8);
+    const int G = gridDim.x, bid = blockIdx.x;
+    // consecutive ranges (consecutive tiles: the row tiles of one W stripe) on one XCD
+    const int w = (G % 8 == 0) ? (bid & 7) * (G / 8) + (bid >> 3) : bid;
+    const long p1 = (long)(w + 1) * d.TP / G;
+    auto slot_rsrc = [&](int tile, int slot) {  // one 256 KB partial slot (wave-uniform)
+        return __builtin_amdgcn_make_buffer_rsrc(a.sk_slab + ((size_t)tile * a.sk_pmax + slot) * kTile * kTile, (short)0,
+                                                 kTile * kTile * 4, 0x00020000);
+    };
+    __shared__ int ok_s[8];
+    // a range shorter than a tile (T < G) meets at most two tiles: the piece (seg) of each
+    auto seg = [&](long p) {
+        f4v acc[2][2][4][2];
+        const int tile = (int)(p / d.U2);
+        const int s = (int)(p - (long)tile * d.U2);
+        const int e = (int)min((long)d.U2, p1 - (long)tile * d.U2);
+        const int vs = 2 * s, ve = 2 * e;
+        const int nhi = max(0, min(ve, d.NH) - vs), lo0 = max(vs, d.NH) - d.NH, nlo = max(0, ve - max(vs, d.NH));
+        const int rt = tile % d.m_tiles, ct = tile / d.m_tiles, m0 = rt * kTile;
+        const int owner = sk_wg_of((long)tile * d.U2, d.TP, G);
+        if (s > 0) {  // a later piece of the tile: slot w - owner - 1, then its flag
+            zero_acc(acc);
+            g3_run<EPI>(a, lds, m0, ct, vs, nhi, lo0, nlo, acc);
+            const int sl = w - owner - 1;
+            // payload written through (sc1) by buffer stores: one SGPR offset per quadrant
+            // instead of 32 64-bit addresses, and no release fence (guide R1 hand-off)
+            const auto rs = slot_rsrc(tile, sl);
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, acc[x][y][i][j]), rs, t * 16,
+                                                                   (((x * 2 + y) * 4 + i) * 2 + j) * kT * 16, 16);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, then one flag
+            __syncthreads();
+            if (t == 0)
+                __hip_atomic_store(a.sk_flags + tile * a.sk_pmax + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            zero_acc(acc);
+            g3_run<EPI>(a, lds, m0, ct, 0, nhi, lo0, nlo, acc);  // a tile's head: from K tile 0
+            const int np = sk_wg_of((long)tile * d.U2 + d.U2 - 1, d.TP, G) - w;  // later pieces
+            if (np > 0) {
+                if (t == 0) {
+                    for (int sl = 0; sl < np; ++sl) {
+                        unsigned* f = a.sk_flags + tile * a.sk_pmax + sl;
+                        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                        int ok = 1;
+                        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                            __builtin_amdgcn_s_sleep(2);
+                            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+                                if (a.err) atomicOr(a.err, 16);
+                                ok = 0;
+                                break;
+                            }
+                        }
+                        ok_s[sl] = ok;
+                        __hip_atomic_store(f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one L2 invalidate, then the barrier
+                }
+                __syncthreads();
+                for (int sl = 0; sl < np; ++sl) {
+                    if (!ok_s[sl]) continue;
+                    const auto rs = slot_rsrc(tile, sl);
+#pragma unroll
+                    for (int x = 0; x < 2; ++x)
+#pragma unroll
+                        for (int y = 0; y < 2; ++y) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                                for (int j = 0; j < 2; ++j)
+                                    acc[x][y][i][j] += __builtin_bit_cast(
+                                        f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, t * 16,
+                                                                                   (((x * 2 + y) * 4 + i) * 2 + j) * kT * 16, 0));
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep the epilogue's address math out of the adds
+            g3_epilogue<EPI>(a, lds, acc, m0, ct, 0);
+            __syncthreads();  // the epilogue's LDS image is read before the next piece's DMA
+        }
+        return (long)tile * d.U2 + e;
+    };
+    const long p0 = (long)w * d.TP / G;
+    if (p0 >= p1) return;
+    const long pn = seg(p0);
+    if (pn < p1) seg(pn);
+}
+
 template <int EPI>
 int launch_g3(const Gemm2Args& a, int grid, hipStream_t s) {
     static const bool attr = [] {
@@ -519,6 +645,18 @@ int launch_g3(const Gemm2Args& a, int grid, hipStream_t s) {
     }();
     LLMI_REQUIRE(attr, "gemm3: cannot raise the dynamic LDS limit");
     hipLaunchKernelGGL(gemm3_kernel<EPI>, dim3(grid), dim3(kT), kLds, s, a);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+template <int EPI>
+int launch_sk(const Gemm2Args& a, hipStream_t s) {
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_sk_kernel<EPI>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess;
+    }();
+    LLMI_REQUIRE(attr, "gemm3: cannot raise the dynamic LDS limit");
+    hipLaunchKernelGGL(gemm3_sk_kernel<EPI>, dim3(a.sk_grid), dim3(kT), kLds, s, a);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }
@@ -592,6 +730,25 @@ size_t gemm3_bal_slab_bytes(int m, int n) {
     return tiles * 2 * kTile * kTile * sizeof(float);
 }
 
+Gemm3SkPlan gemm3_sk_plan(int m, int n, int k, int epi, int planes, int lo8, int g) {
+    Gemm3SkPlan p;
+    if ((epi != EPI_STORE && epi != EPI_SILU_MUL) || m <= 0 || g <= 0 || !gemm3_supported(n, k, epi, 1)) return p;
+    if (lo8 && k % (2 * kK) != 0) return p;
+    const int n_tiles = (epi == EPI_SILU_MUL) ? (n / 2) / 128 : n / kTile;
+    const SkDims d = sk_dims(m, n_tiles, k, planes, lo8);
+    const int NL = planes == 2 ? (lo8 ? k / (2 * kK) : k / kK) : 0;
+    // pairs never straddle the hi / lo boundary; >= 2 pairs a workgroup
+    if (d.T >= g || d.TP < 2L * g || d.NH % 2 != 0 || NL % 2 != 0) return p;
+    int pmax = 0;
+    for (int t = 0; t < d.T; ++t)
+        pmax = std::max(pmax, sk_wg_of((long)t * d.U2 + d.U2 - 1, d.TP, g) - sk_wg_of((long)t * d.U2, d.TP, g));
+    if (pmax < 1 || pmax > 8) return p;
+    p.pmax = pmax;
+    p.slab_bytes = (size_t)d.T * pmax * kTile * kTile * sizeof(float);
+    p.flag_bytes = (size_t)d.T * pmax * sizeof(unsigned);
+    return p;
+}
+
 bool gemm3_supported(int n, int k, int epi, int ksplit) {
     const int ncols = (epi == EPI_SILU_MUL) ? n / 2 : n;
     const int tile = (epi == EPI_SILU_MUL) ? 128 : kTile;
@@ -655,6 +812,13 @@ int gemm3_launch(Gemm2Args a, hipStream_t s) {
             LLMI_HIP(hipGetLastError());
             return LLMI_OK;
         }
+    }
+    if (a.sk_slab && a.sk_flags && a.sk_grid > 0 && (a.epi == EPI_STORE || a.epi == EPI_SILU_MUL)) {
+        const Gemm3SkPlan p = gemm3_sk_plan(a.m, a.n, a.k, a.epi, a.planes, a.lo8, a.sk_grid);
+        LLMI_REQUIRE(p.pmax > 0, "gemm3: stream-K requested for a shape it does not cover (see gemm3_sk_plan)");
+        a.sk_pmax = p.pmax;
+        if (a.epi == EPI_STORE) return launch_sk<EPI_STORE>(a, s);
+        return launch_sk<EPI_SILU_MUL>(a, s);
     }
     switch (a.epi) {
         case EPI_STORE: return launch_g3<EPI_STORE>(a, grid, s);

@@ -131,7 +131,26 @@ struct Gemm2Args {
     int bal_own = 0;               // set by gemm3_launch: lo tile pairs each owner keeps
     int* err = nullptr;
     unsigned long long* stamps = nullptr;  // debug timeline of the balanced kernel (WgStamp), null = off            // sticky error word (bit 16: a lo partial never arrived)
+    // gemm3 stream-K (EPI_STORE / EPI_SILU_MUL with fewer 256 x 256 tiles than CUs; see
+    // gemm3_sk_kernel): sk_grid workgroups (<= the CU count) share the tiles' K work evenly;
+    // a tile's later pieces go to fp32 partial slots [tiles][sk_pmax][256 x 256] and set flags
+    // [tiles][sk_pmax] (zeroed once; the tile's first workgroup resets each after reading)
+    float* sk_slab = nullptr;
+    unsigned* sk_flags = nullptr;
+    int sk_grid = 0;
+    int sk_pmax = 0;
 };
+// stream-K plan for gemm3 (m rows, n columns -- gate_up: 2 x inter --, k, planes / lo8 as in
+// Gemm2Args) on g workgroups: slots per tile (0: stream-K does not apply), and the bytes of
+// partial slots and of flags it needs
+struct Gemm3SkPlan {
+    int pmax = 0;
+    size_t slab_bytes = 0, flag_bytes = 0;
+};
+Gemm3SkPlan gemm3_sk_plan(int m, int n, int k, int epi, int planes, int lo8, int g);
+// attach the stream-K workspace (per device and stream, gemm2.hip) to a gemm3 launch of g's
+// shape when the plan keeps <= 3 slots a tile; false: launch as before (LLMI_SK=0: never)
+bool gemm3_sk_attach(Gemm2Args& g, hipStream_t s);
 // bytes of the balanced gate_up's partial slots for m rows, n = 2 x intermediate (0: not used)
 size_t gemm3_bal_slab_bytes(int m, int n);
 // e4m3(W * 2^exp) of an fp16 [rows, cols] weight (exp chosen so that max |W| * 2^exp <= 448),

@@ -449,3 +449,41 @@ def test_context_attention_proj_matches_linear_then_qkv(ops, cache_dt, lens, his
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(N(k1), N(k2))
     np.testing.assert_array_equal(N(v1), N(v2))
+
+
+def test_linear_stream_k_shape_matches_fp64(ops):
+    """A projection whose 256 x 256 tiles leave CUs idle (m 512, n 12288: 96 tiles) runs on
+    gemm3's stream-K form (gemm3_sk_kernel: equal K ranges per workgroup across tiles, later
+    pieces through partial slots added in order by the tile's first workgroup): against
+    float64 within llmi_linear's 1e-5, twice in a row bitwise equal (repeatable sums, the
+    slot flags reset for the next launch), and as the residual form."""
+    rng = np.random.default_rng(31)
+    m, n, k = 512, 12288, 1024
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    w = (rng.standard_normal((n, k)) / math.sqrt(k)).astype(np.float16)
+    y1 = N(ops.launchLinearGemm(T(x), T(w)))
+    y2 = N(ops.launchLinearGemm(T(x), T(w)))
+    np.testing.assert_array_equal(y1, y2)
+    want = x.astype(np.float64) @ w.astype(np.float64).T
+    e = rel(y1, want)
+    print(f"stream-K linear {m}x{n}x{k}: rel-L2 vs fp64 {e:.2e}")
+    assert e < 1e-5
+
+
+def test_ffn_stream_k_shape_matches_fp64(ops):
+    """llmi_ffn with a gate_up of 96 tiles (m 512, inter 6144): the SiLU*up epilogue after the
+    stream-K sum, against float64 within 1e-5, repeatable bitwise."""
+    rng = np.random.default_rng(32)
+    m, hidden, inter = 512, 1024, 6144
+    x = rng.standard_normal((m, hidden)).astype(np.float32)
+    wgu = (rng.standard_normal((2 * inter, hidden)) / math.sqrt(hidden)).astype(np.float16)
+    wd = (rng.standard_normal((hidden, inter)) / math.sqrt(inter)).astype(np.float16)
+    got = N(ops.ffn(T(x), T(wgu), T(wd)))
+    np.testing.assert_array_equal(got, N(ops.ffn(T(x), T(wgu), T(wd))))
+    x64, g64, d64 = x.astype(np.float64), wgu.astype(np.float64), wd.astype(np.float64)
+    gu = x64 @ g64.T
+    g, u = gu[:, :inter], gu[:, inter:]
+    want = ((g / (1.0 + np.exp(-g))) * u) @ d64.T
+    e = rel(got, want)
+    print(f"stream-K ffn m {m} hidden {hidden} inter {inter}: rel-L2 vs fp64 {e:.2e}")
+    assert e < 1e-5
