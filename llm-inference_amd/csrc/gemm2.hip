@@ -41,6 +41,14 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
+// LLMI_RN256=1: the row kernels (rows_split, resid_norm) at 256 threads a row instead of 1024 (A/B)
+inline bool noexp_rn() {
+    static const bool v = [] {
+        const char* e = std::getenv("LLMI_RN256");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
 constexpr int kBN = 128;
 constexpr int kBK = 64;
 constexpr int kRowB = kBK * 2;  // 128-B LDS rows
@@ -222,17 +230,17 @@ __global__ __launch_bounds__(kThreads) void gemm2_kernel(Gemm2Args a) {
 // per thread, k <= NPT * 1024): x and the slab slices are read once, x written once.
 // KS > 0: the slice count is a constant and every slice's loads are issued before the
 // first add (one memory round trip instead of one per slice); KS = 0: runtime ksplit.
-template <int NPT, int KS>
-__global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx, int k, const void* gamma,
-                                                             int g_dtype, float eps, _Float16* hi, _Float16* lo,
-                                                             int ldh, const float* slab, int ksplit, int m, int lo8) {
+template <int NPT, int KS, int BS = kThreads>
+__global__ __launch_bounds__(BS) void rows_split_kernel(float* x, int ldx, int k, const void* gamma,
+                                                       int g_dtype, float eps, _Float16* hi, _Float16* lo,
+                                                       int ldh, const float* slab, int ksplit, int m, int lo8) {
     __shared__ float red[16];
     float* xr = x + (size_t)blockIdx.x * ldx;
     const int k4 = k / 4;
     float4 v[NPT];
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
-        const int j = threadIdx.x + i * kThreads;
+        const int j = threadIdx.x + i * BS;
         v[i] = j < k4 ? reinterpret_cast<const float4*>(xr)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (KS > 0 && slab) {  // split-K combine: x += slice 0 + slice 1 + ... (fixed order)
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
             const float4* sl = reinterpret_cast<const float4*>(slab + ((size_t)s * m + blockIdx.x) * ldx);
 #pragma unroll
             for (int i = 0; i < NPT; ++i) {
-                const int j = threadIdx.x + i * kThreads;
+                const int j = threadIdx.x + i * BS;
                 p[s][i] = j < k4 ? sl[j] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
@@ -257,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
             const float4* sl = reinterpret_cast<const float4*>(slab + ((size_t)s * m + blockIdx.x) * ldx);
 #pragma unroll
             for (int i = 0; i < NPT; ++i) {
-                const int j = threadIdx.x + i * kThreads;
+                const int j = threadIdx.x + i * BS;
                 if (j < k4) {
                     const float4 p = sl[j];
                     v[i].x += p.x; v[i].y += p.y; v[i].z += p.z; v[i].w += p.w;
@@ -268,7 +276,7 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
     if (slab) {  // x written back
 #pragma unroll
         for (int i = 0; i < NPT; ++i) {
-            const int j = threadIdx.x + i * kThreads;
+            const int j = threadIdx.x + i * BS;
             if (j < k4) reinterpret_cast<float4*>(xr)[j] = v[i];
         }
         if (!hi) return;
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void rows_split_kernel(float* x, int ldx,
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
-        const int j = threadIdx.x + i * kThreads;
+        const int j = threadIdx.x + i * BS;
         if (j >= k4) continue;
         float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
         if (gamma) {
@@ -401,7 +409,17 @@ int rows_split_launch(float* x, int ldx, int m, int k, const void* gamma, int g_
         else                              \
             RS_LAUNCH(N, 0);              \
     } while (0)
-    if (npt <= 4)
+    if (k / 4 <= 1024 && !noexp_rn()) {  // one float4 per thread: 16 waves a row (resid_norm's A/B)
+        if (ks == 2)
+            hipLaunchKernelGGL((rows_split_kernel<1, 2, 1024>), dim3(m), dim3(1024), 0, s, x, ldx, k, gamma, g_dtype, eps,
+                               hi, lo, ldh, slab, ksplit, m, lo8 ? 1 : 0);
+        else if (ks == 8)
+            hipLaunchKernelGGL((rows_split_kernel<1, 8, 1024>), dim3(m), dim3(1024), 0, s, x, ldx, k, gamma, g_dtype, eps,
+                               hi, lo, ldh, slab, ksplit, m, lo8 ? 1 : 0);
+        else
+            hipLaunchKernelGGL((rows_split_kernel<1, 0, 1024>), dim3(m), dim3(1024), 0, s, x, ldx, k, gamma, g_dtype, eps,
+                               hi, lo, ldh, slab, ksplit, m, lo8 ? 1 : 0);
+    } else if (npt <= 4)
         RS_KS(4);
     else if (npt <= 5)
         RS_KS(5);
@@ -450,9 +468,9 @@ __global__ __launch_bounds__(kThreads) void slab_sum_kernel(const float4* slab, 
 // order), r = resid + t (add_resid_rmsnorm_kernel's / add_resid_kernel's order), then the
 // row's RMSNorm * gamma -- the launchLinearGemm + launchFusedAddBiasResidualRMSNorm pair
 // (or + launchAddResidual + the next layer's launchRMSNorm) in one pass over the slices.
-template <int NPT>
-__global__ __launch_bounds__(kThreads) void resid_norm_kernel(float* resid, const float* slab, int ks, int m, int n,
-                                                              float* out, const void* gamma, int g_dtype, float eps) {
+template <int NPT, int BS = kThreads>
+__global__ __launch_bounds__(BS) void resid_norm_kernel(float* resid, const float* slab, int ks, int m, int n,
+                                                        float* out, const void* gamma, int g_dtype, float eps) {
     __shared__ float red[16];
     const size_t row = blockIdx.x;
     const int n4 = n / 4;
@@ -465,7 +483,7 @@ __global__ __launch_bounds__(kThreads) void resid_norm_kernel(float* resid, cons
     // 512 x 4096: the slice-at-a-time loop below keeps more rows in flight per CU)
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
-        const int j = threadIdx.x + i * kThreads;
+        const int j = threadIdx.x + i * BS;
         v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (j >= n4) continue;
         float4 t = sl[j];
@@ -487,7 +505,7 @@ __global__ __launch_bounds__(kThreads) void resid_norm_kernel(float* resid, cons
     float4* o = reinterpret_cast<float4*>(out) + row * n4;
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
-        const int j = threadIdx.x + i * kThreads;
+        const int j = threadIdx.x + i * BS;
         if (j >= n4) continue;
         float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
         if (gamma) {
@@ -503,7 +521,10 @@ __global__ __launch_bounds__(kThreads) void resid_norm_kernel(float* resid, cons
 }
 int resid_norm_launch(const ResidEpi& re, const float* slab, int ks, int m, int n, hipStream_t s) {
     const int npt = (n / 4 + kThreads - 1) / kThreads;
-    if (npt <= 4)
+    if (n / 4 <= 1024 && !noexp_rn())  // one float4 per thread: 16 waves a row keep more loads in flight
+        hipLaunchKernelGGL((resid_norm_kernel<1, 1024>), dim3(m), dim3(1024), 0, s, re.resid, slab, ks, m, n, re.out,
+                           re.gamma, re.g_dtype, re.eps);
+    else if (npt <= 4)
         hipLaunchKernelGGL(resid_norm_kernel<4>, dim3(m), dim3(kThreads), 0, s, re.resid, slab, ks, m, n, re.out,
                            re.gamma, re.g_dtype, re.eps);
     else
