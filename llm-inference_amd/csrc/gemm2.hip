@@ -636,9 +636,17 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
     const bool g3 = m >= 256 && gemm3_supported(n, k, EPI_STORE, 1);
     const int tiles = g3 ? ((m + 255) / 256) * (n / 256) : ((m + 127) / 128) * (n / kBN);
     // (stream-K measured slower here than the 2-slice split: q/k/v 112 vs ~108 us with the
-    // slices' sum, its 256-KB partial slots being on the critical path; gate_up gains)
+    // slices' sum, its 256-KB partial slots being on the critical path; gate_up gains.
+    // LLMI_SK_LINEAR=1 turns it on for these projections, for A/B)
+    static const bool sk_lin = [] {
+        const char* e = std::getenv("LLMI_SK_LINEAR");
+        return e && e[0] == '1';
+    }();
+    Gemm2Args skg;
+    skg.m = m; skg.n = n; skg.k = k; skg.planes = 2; skg.epi = EPI_STORE;
+    const bool sk = sk_lin && g3 && sk_setup(skg, s);
     int ks = 1;  // K slices while the tiles leave more than a third of the 256 CUs idle
-    while (tiles * ks < 160 && ks < 8) {
+    while (!sk && tiles * ks < 160 && ks < 8) {
         const int nk = ks * 2;
         if (g3 ? !gemm3_supported(n, k, EPI_SLAB, nk) : k % (nk * kBK) != 0) break;
         ks = nk;
@@ -657,6 +665,7 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
     Gemm2Args g;
     g.a[0] = hi; g.a[1] = lo; g.planes = 2; g.lda = k;
     g.w = w; g.m = m; g.n = n; g.k = k; g.ldy = n;
+    if (sk) { g.sk_slab = skg.sk_slab; g.sk_flags = skg.sk_flags; g.sk_grid = skg.sk_grid; }
     float* sl = reinterpret_cast<float*>(ws + 2 * plane);
     if (ks > 1) {
         g.epi = EPI_SLAB; g.ksplit = ks; g.slab = sl; g.y = re || raw ? sl : y;

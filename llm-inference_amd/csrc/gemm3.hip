@@ -522,6 +522,9 @@ __global__ __launch_bounds__(kT) void gemm3_silu_bal_kernel(Gemm2Args a) {
 // (bounded: error bit 16), resets them (a graph replay finds them zero), adds the slots in
 // order onto its own piece (repeatable sums) and runs the tile's epilogue. Every workgroup
 // is resident (sk_grid <= the CU count, one 136-KB workgroup per CU), so waits always end.
+#ifndef LLMI_SK_EXP
+#define LLMI_SK_EXP 0  // timing-only builds: 1 = flags without the slot payload, 2 = no hand-off at all
+#endif
 struct SkDims {
     int m_tiles, T, NH, U2;
     long TP;
@@ -544,9 +547,14 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
     const int t = threadIdx.x;
     const SkDims d = sk_dims(a.m, a.n_tiles, a.k, a.planes, a.lo8);
     const int G = gridDim.x, bid = blockIdx.x;
-    // consecutive ranges (consecutive tiles: the row tiles of one W stripe) on one XCD
+    // consecutive workgroups on one XCD; workgroup w = v * m_tiles + rt: the m_tiles row tiles
+    // of a W column stripe get the SAME K ranges from sibling workgroups running side by side,
+    // so each W chunk is read once into the XCD's L2 for all of them (ranges cut per tile made
+    // the siblings read different K at the same time: W read twice, 179 vs ~145 us at gate_up)
     const int w = (G % 8 == 0) ? (bid & 7) * (G / 8) + (bid >> 3) : bid;
-    const long p1 = (long)(w + 1) * d.TP / G;
+    const int MT = d.m_tiles, Gp = G / MT, v = w / MT, rt = w % MT;
+    const long TPs = (long)a.n_tiles * d.U2;  // pairs of all column stripes
+    const long p1 = (long)(v + 1) * TPs / Gp;
     auto slot_rsrc = [&](int tile, int slot) {  // one 256 KB partial slot (wave-uniform)
         return __builtin_amdgcn_make_buffer_rsrc(a.sk_slab + ((size_t)tile * a.sk_pmax + slot) * kTile * kTile, (short)0,
                                                  kTile * kTile * 4, 0x00020000);
@@ -555,17 +563,17 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
     // a range shorter than a tile (T < G) meets at most two tiles: the piece (seg) of each
     auto seg = [&](long p) {
         f4v acc[2][2][4][2];
-        const int tile = (int)(p / d.U2);
-        const int s = (int)(p - (long)tile * d.U2);
-        const int e = (int)min((long)d.U2, p1 - (long)tile * d.U2);
+        const int ct = (int)(p / d.U2);
+        const int s = (int)(p - (long)ct * d.U2);
+        const int e = (int)min((long)d.U2, p1 - (long)ct * d.U2);
         const int vs = 2 * s, ve = 2 * e;
         const int nhi = max(0, min(ve, d.NH) - vs), lo0 = max(vs, d.NH) - d.NH, nlo = max(0, ve - max(vs, d.NH));
-        const int rt = tile % d.m_tiles, ct = tile / d.m_tiles, m0 = rt * kTile;
-        const int owner = sk_wg_of((long)tile * d.U2, d.TP, G);
-        if (s > 0) {  // a later piece of the tile: slot w - owner - 1, then its flag
+        const int tile = ct * MT + rt, m0 = rt * kTile;
+        const int owner = sk_wg_of((long)ct * d.U2, TPs, Gp);  // in units of sibling groups
+        if (s > 0) {  // a later piece of the tile: slot v - owner - 1, then its flag
             zero_acc(acc);
             g3_run<EPI>(a, lds, m0, ct, vs, nhi, lo0, nlo, acc);
-            const int sl = w - owner - 1;
+            const int sl = v - owner - 1;
             // payload written through (sc1) by buffer stores: one SGPR offset per quadrant
             // instead of 32 64-bit addresses, and no release fence (guide R1 hand-off)
             const auto rs = slot_rsrc(tile, sl);
@@ -577,16 +585,16 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
                     for (int i = 0; i < 4; ++i)
 #pragma unroll
                         for (int j = 0; j < 2; ++j)
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, acc[x][y][i][j]), rs, t * 16,
+                            if (LLMI_SK_EXP == 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, acc[x][y][i][j]), rs, t * 16,
                                                                    (((x * 2 + y) * 4 + i) * 2 + j) * kT * 16, 16);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, then one flag
             __syncthreads();
-            if (t == 0)
+            if (t == 0 && LLMI_SK_EXP != 2)
                 __hip_atomic_store(a.sk_flags + tile * a.sk_pmax + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             zero_acc(acc);
             g3_run<EPI>(a, lds, m0, ct, 0, nhi, lo0, nlo, acc);  // a tile's head: from K tile 0
-            const int np = sk_wg_of((long)tile * d.U2 + d.U2 - 1, d.TP, G) - w;  // later pieces
+            const int np = LLMI_SK_EXP == 2 ? 0 : sk_wg_of((long)ct * d.U2 + d.U2 - 1, TPs, Gp) - v;  // later pieces
             if (np > 0) {
                 if (t == 0) {
                     for (int sl = 0; sl < np; ++sl) {
@@ -608,7 +616,7 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
                 }
                 __syncthreads();
                 for (int sl = 0; sl < np; ++sl) {
-                    if (!ok_s[sl]) continue;
+                    if (!ok_s[sl] || LLMI_SK_EXP == 1) continue;
                     const auto rs = slot_rsrc(tile, sl);
 #pragma unroll
                     for (int x = 0; x < 2; ++x)
@@ -629,9 +637,10 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
             g3_epilogue<EPI>(a, lds, acc, m0, ct, 0);
             __syncthreads();  // the epilogue's LDS image is read before the next piece's DMA
         }
-        return (long)tile * d.U2 + e;
+        return (long)ct * d.U2 + e;
     };
-    const long p0 = (long)w * d.TP / G;
+    if (v >= Gp) return;  // G not a multiple of m_tiles: the spare workgroups
+    const long p0 = (long)v * TPs / Gp;
     if (p0 >= p1) return;
     const long pn = seg(p0);
     if (pn < p1) seg(pn);
@@ -737,11 +746,13 @@ Gemm3SkPlan gemm3_sk_plan(int m, int n, int k, int epi, int planes, int lo8, int
     const int n_tiles = (epi == EPI_SILU_MUL) ? (n / 2) / 128 : n / kTile;
     const SkDims d = sk_dims(m, n_tiles, k, planes, lo8);
     const int NL = planes == 2 ? (lo8 ? k / (2 * kK) : k / kK) : 0;
+    const int gp = g / d.m_tiles;  // sibling groups: one workgroup per row tile
+    const long tps = (long)n_tiles * d.U2;
     // pairs never straddle the hi / lo boundary; >= 2 pairs a workgroup
-    if (d.T >= g || d.TP < 2L * g || d.NH % 2 != 0 || NL % 2 != 0) return p;
+    if (d.T >= g || gp < 1 || tps < 2L * gp || d.NH % 2 != 0 || NL % 2 != 0) return p;
     int pmax = 0;
-    for (int t = 0; t < d.T; ++t)
-        pmax = std::max(pmax, sk_wg_of((long)t * d.U2 + d.U2 - 1, d.TP, g) - sk_wg_of((long)t * d.U2, d.TP, g));
+    for (int c = 0; c < n_tiles; ++c)
+        pmax = std::max(pmax, sk_wg_of((long)c * d.U2 + d.U2 - 1, tps, gp) - sk_wg_of((long)c * d.U2, tps, gp));
     if (pmax < 1 || pmax > 8) return p;
     p.pmax = pmax;
     p.slab_bytes = (size_t)d.T * pmax * kTile * kTile * sizeof(float);
