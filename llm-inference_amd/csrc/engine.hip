@@ -1091,9 +1091,9 @@ struct Engine {
         // (o slices into x) + rmsnorm + gate_up + silu * up -> planes of the down GEMM's input
         LLMI_TRY(rows_split_launch(pf_x, H, m, H, L.ffn_norm, edt, c.rms_eps, pf_ah, lo, H, stream, pf_slab, so, f8));
         g.lda = H; g.w = L.gu; g.n = 2 * il; g.k = H;
-        static const bool sk_f8 = [] {  // fp8-lo gate_up: stream-K instead of the lo-pass balance
+        static const bool sk_f8 = [] {  // fp8-lo gate_up: stream-K (LLMI_SK_F8=0: the lo-pass balance)
             const char* e = std::getenv("LLMI_SK_F8");
-            return e && std::string(e) == "1";
+            return !(e && std::string(e) == "0");
         }();
         if (f8) {  // + the fp8 lo pass spread over the CUs its 256 x 256 tiles leave idle (the
                    // fp16 lo pass balanced the same way measured 231 vs 225 us: not used)
