@@ -11,6 +11,7 @@
 // All are memory-bound element moves or row reductions (fp32 arithmetic, T = float
 // or __half storage); roofline HBM, bytes = what they read + write.
 #include <cfloat>
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernels.h"
@@ -168,7 +169,7 @@ __global__ void rope_qkv_prefill_kernel(const T* qkv, T* q_buf, T* k_buf, T* v_b
 // the projection ks_stride floats apart (llmi_context_attention_proj): they are summed in
 // slice order on the load, slab_sum_kernel's order, so the values are the same bits.
 template <typename KT>
-__global__ __launch_bounds__(256) void rope_qkv_cache_tok_kernel(const float* qkv, float* q_buf, KT* k_cache,
+__global__ __launch_bounds__(1024) void rope_qkv_cache_tok_kernel(const float* qkv, float* q_buf, KT* k_cache,
                                                                  KT* v_cache, const int* po, const int* hist,
                                                                  int seq_len, int heads, int kv_heads, float base,
                                                                  int max_seq, int ks, size_t ks_stride) {
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_tok_kernel(const float* qk
         hi = make_float4(rot_hi(x0.x, x1.x, c.x, sn.x), rot_hi(x0.y, x1.y, c.y, sn.y), rot_hi(x0.z, x1.z, c.z, sn.z),
                          rot_hi(x0.w, x1.w, c.w, sn.w));
     };
-    for (int e = t; e < heads * d4; e += 256) {  // q heads
+    for (int e = t; e < heads * d4; e += (int)blockDim.x) {  // q heads
         const int h = e / d4, j = e % d4;
         float4 lo, hi;
         rot4(row + (size_t)h * d, j, lo, hi);
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_tok_kernel(const float* qk
             dst[0] = __float2half(v.x); dst[1] = __float2half(v.y); dst[2] = __float2half(v.z); dst[3] = __float2half(v.w);
         }
     };
-    for (int e = t; e < kv_heads * d4; e += 256) {  // k heads into the cache slot
+    for (int e = t; e < kv_heads * d4; e += (int)blockDim.x) {  // k heads into the cache slot
         const int h = e / d4, j = e % d4;
         float4 lo, hi;
         rot4(row + (size_t)(heads + h) * d, j, lo, hi);
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_tok_kernel(const float* qk
         st4(ko + 4 * j, lo);
         st4(ko + d / 2 + 4 * j, hi);
     }
-    for (int e = t; e < kv_heads * (d / 4); e += 256) {  // v heads
+    for (int e = t; e < kv_heads * (d / 4); e += (int)blockDim.x) {  // v heads
         const int h = e / (d / 4), j = e % (d / 4);
         const float4 v = ld4(row + (size_t)(heads + kv_heads + h) * d + 4 * j);
         st4(v_cache + (((size_t)b * kv_heads + h) * max_seq + pos) * d + 4 * j, v);
@@ -234,6 +235,16 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_tok_kernel(const float* qk
 }
 
 bool fp_dtype(int dt) { return dt == LLMI_F32 || dt == LLMI_F16; }
+// workgroup size of the per-token RoPE kernels (LLMI_ROPE_THREADS, A/B; default 1024: more
+// loads in flight a token, as the row kernels)
+int rope_threads() {
+    static const int v = [] {
+        const char* e = std::getenv("LLMI_ROPE_THREADS");
+        const int n = e ? std::atoi(e) : 1024;
+        return (n == 256 || n == 512 || n == 1024) ? n : 1024;
+    }();
+    return v;
+}
 
 }  // namespace
 
@@ -731,11 +742,11 @@ int context_attention_qkv_launch(const float* qkv, const int* padding_offset, co
                      (reinterpret_cast<uintptr_t>(k_cache) & 7) == 0 && (reinterpret_cast<uintptr_t>(v_cache) & 7) == 0,
                  "context_attention_qkv: qkv and q_scratch 16-B, the caches 8-B aligned");
     if (cache_dtype == LLMI_F32)
-        hipLaunchKernelGGL(rope_qkv_cache_tok_kernel<float>, dim3(num_tokens), dim3(256), 0, s, qkv, q_scratch,
+        hipLaunchKernelGGL(rope_qkv_cache_tok_kernel<float>, dim3(num_tokens), dim3(rope_threads()), 0, s, qkv, q_scratch,
                            (float*)k_cache + off, (float*)v_cache + off, padding_offset, history_length, max_q,
                            heads, kv_heads, rope_base, max_seq, ks, ks_stride);
     else
-        hipLaunchKernelGGL(rope_qkv_cache_tok_kernel<__half>, dim3(num_tokens), dim3(256), 0, s, qkv, q_scratch,
+        hipLaunchKernelGGL(rope_qkv_cache_tok_kernel<__half>, dim3(num_tokens), dim3(rope_threads()), 0, s, qkv, q_scratch,
                            (__half*)k_cache + off, (__half*)v_cache + off, padding_offset, history_length, max_q,
                            heads, kv_heads, rope_base, max_seq, ks, ks_stride);
     LLMI_HIP(hipGetLastError());

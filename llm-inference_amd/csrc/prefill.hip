@@ -240,6 +240,15 @@ constexpr int KB = 64;  // keys per block
 // chunk writes its output directly; otherwise every chunk writes its unnormalised
 // (O, m, l) to ws[head][qb][chunk] and attn_prefill_merge_kernel combines them in
 // chunk order. blockIdx.x enumerates (qb, chunk), longest query blocks first.
+// workgroup size of rope_kv_prefill_kernel (LLMI_ROPE_THREADS, A/B; default 1024)
+inline int pf_rope_threads() {
+    static const int v = [] {
+        const char* e = std::getenv("LLMI_ROPE_THREADS");
+        const int n = e ? std::atoi(e) : 1024;
+        return (n == 256 || n == 512 || n == 1024) ? n : 1024;
+    }();
+    return v;
+}
 __host__ __device__ inline int pf_nkb(int qb, int p0, int m_rows) {
     const int kend = p0 + (qb * QM + QM < m_rows ? qb * QM + QM : m_rows);
     return (kend + KB - 1) / KB;
@@ -612,7 +621,7 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
     const int ld = (a.heads + 2 * a.kv_heads) * D;
     const dim3 ga((a.m + QB - 1) / QB, a.heads);
     if (a.cache_dtype == LLMI_F16) {
-        hipLaunchKernelGGL(rope_kv_prefill_kernel<__half>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
+        hipLaunchKernelGGL(rope_kv_prefill_kernel<__half>, dim3(a.m), dim3(pf_rope_threads()), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (__half*)a.k_cache, (__half*)a.v_cache, a.max_seq);
         if (a.mfma_planes) {
             // split keys: chunks of cb key blocks
@@ -664,7 +673,7 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
                                a.heads * D);
         }
     } else if (a.cache_dtype == LLMI_F32) {
-        hipLaunchKernelGGL(rope_kv_prefill_kernel<float>, dim3(a.m), dim3(kThreads), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
+        hipLaunchKernelGGL(rope_kv_prefill_kernel<float>, dim3(a.m), dim3(pf_rope_threads()), 0, s, a.qkv, a.qkv2, ld, a.p0, a.heads,
                            a.kv_heads, a.rope_tab, (float*)a.k_cache, (float*)a.v_cache, a.max_seq);
         hipLaunchKernelGGL(attn_prefill_kernel<float>, ga, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0, a.heads,
                            a.kv_heads, (const float*)a.k_cache, (const float*)a.v_cache, a.max_seq, a.out,
