@@ -452,11 +452,10 @@ def test_context_attention_proj_matches_linear_then_qkv(ops, cache_dt, lens, his
 
 
 def test_linear_stream_k_shape_matches_fp64(ops):
-    """A projection whose 256 x 256 tiles leave CUs idle (m 512, n 12288: 96 tiles) runs on
-    gemm3's stream-K form (gemm3_sk_kernel: equal K ranges per workgroup across tiles, later
-    pieces through partial slots added in order by the tile's first workgroup): against
-    float64 within llmi_linear's 1e-5, twice in a row bitwise equal (repeatable sums, the
-    slot flags reset for the next launch), and as the residual form."""
+    """A q/k/v-shaped projection whose 256 x 256 tiles leave CUs idle (m 512, n 12288: 96
+    tiles): on the 2-slice split by default (stream-K measured slower for q/k/v; with
+    LLMI_SK_LINEAR=1 the same call takes gemm3_sk_kernel): against float64 within
+    llmi_linear's 1e-5 and twice in a row bitwise equal (repeatable sums)."""
     rng = np.random.default_rng(31)
     m, n, k = 512, 12288, 1024
     x = rng.standard_normal((m, k)).astype(np.float32)
@@ -486,4 +485,35 @@ def test_ffn_stream_k_shape_matches_fp64(ops):
     want = ((g / (1.0 + np.exp(-g))) * u) @ d64.T
     e = rel(got, want)
     print(f"stream-K ffn m {m} hidden {hidden} inter {inter}: rel-L2 vs fp64 {e:.2e}")
+    assert e < 1e-5
+
+
+def test_ffn_without_stream_k_matches_fp64():
+    """LLMI_SK=0 (the knob that turns gemm3 stream-K off) in a child process: llmi_ffn at the
+    stream-K shape on the plain 172-tile launch, against float64 within the same 1e-5."""
+    import subprocess
+    import sys
+    import os
+    code = r'''
+import math, numpy as np, torch, sys
+sys.path.insert(0, "llm-inference_amd")
+from llmi import ops
+rng = np.random.default_rng(32)
+m, hidden, inter = 512, 1024, 6144
+x = rng.standard_normal((m, hidden)).astype(np.float32)
+wgu = (rng.standard_normal((2 * inter, hidden)) / math.sqrt(hidden)).astype(np.float16)
+wd = (rng.standard_normal((hidden, inter)) / math.sqrt(inter)).astype(np.float16)
+T = lambda a: torch.from_numpy(a).cuda()
+got = ops.ffn(T(x), T(wgu), T(wd)).cpu().numpy().astype(np.float64)
+gu = x.astype(np.float64) @ wgu.astype(np.float64).T
+g, u = gu[:, :inter], gu[:, inter:]
+want = ((g / (1.0 + np.exp(-g))) * u) @ wd.astype(np.float64).T
+print(np.linalg.norm(got - want) / np.linalg.norm(want))
+'''
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LLMI_SK="0")
+    r = subprocess.run([sys.executable, "-c", code], cwd=repo, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    e = float(r.stdout.strip().splitlines()[-1])
+    print(f"ffn with LLMI_SK=0: rel-L2 vs fp64 {e:.2e}")
     assert e < 1e-5
