@@ -114,6 +114,13 @@ int llmi_ffn_residual(const float* x, const void* w_gate_up, const void* w_down,
                       int inter, float* residual, float* out, const void* gamma, int gamma_dtype, float eps,
                       llmi_stream_t stream);
 
+/* Sticky device error bits recorded by launches on `stream` (current device) that have no
+ * error word of their own -- llmi_linear / llmi_ffn / the *_residual calls: 16 = a stream-K
+ * partial never arrived within 2 s (its workgroup could not run alongside the others), so
+ * that output is incomplete. Synchronises the stream, stores the bits in *flags and clears
+ * them. No counterpart in the reference (its cuBLAS calls have no cross-workgroup wait). */
+int llmi_stream_errors(llmi_stream_t stream, int* flags);
+
 /* One decode row through the HBM-streaming GEMV with its fused prologue/epilogue -- what
  * LlamaSelfDecoder::forward strings together for a token (self_decoder.cpp:59-81 fused):
  *   gamma != NULL: x is RMS-normalised and scaled by gamma (dtype gamma_dtype) first;

@@ -104,6 +104,8 @@ int llmi_ffn_residual(const float* x, const void* w_gate_up, const void* w_down,
     return ffn_mfma_launch(x, w_gate_up, w_down, nullptr, m, hidden, inter, STREAM(stream), &re);
 }
 
+int llmi_stream_errors(llmi_stream_t stream, int* flags) { return stream_errors(STREAM(stream), flags); }
+
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
                 llmi_stream_t stream) {
     LLMI_REQUIRE(m >= 1 && n >= 1 && k >= 1, "linear: m, n, k must be >= 1");

@@ -594,6 +594,25 @@ int sk_workspace(hipStream_t s, size_t slab_bytes, size_t flag_bytes, float** sl
     *flags = e.second.first;
     return LLMI_OK;
 }
+// sticky device error bits per (device, stream) for launches whose caller passes no error
+// word (the layer API): allocated once and zeroed, read and cleared by stream_errors()
+std::map<std::pair<int, hipStream_t>, int*> g_err;
+int stream_error_word(hipStream_t s, int** out) {
+    int dev = 0;
+    LLMI_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    int*& e = g_err[{dev, s}];
+    if (!e) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        LLMI_HIP(hipStreamIsCapturing(s, &cap));
+        LLMI_REQUIRE(cap == hipStreamCaptureStatusNone,
+                     "stream error word: first use cannot happen while the stream is capturing");
+        LLMI_HIP(hipMalloc(reinterpret_cast<void**>(&e), sizeof(int)));
+        LLMI_HIP(hipMemsetAsync(e, 0, sizeof(int), s));
+    }
+    *out = e;
+    return LLMI_OK;
+}
 int cu_count() {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -614,12 +633,32 @@ bool sk_setup(Gemm2Args& g, hipStream_t s) {
     const Gemm3SkPlan p = gemm3_sk_plan(g.m, g.n, g.k, g.epi, g.planes, g.lo8, n_cu);
     if (p.pmax < 1 || p.pmax > 3) return false;
     if (sk_workspace(s, p.slab_bytes, p.flag_bytes, &g.sk_slab, &g.sk_flags) != LLMI_OK) return false;
+    // a partial that never arrives sets bit 16 somewhere the caller can read (stream_errors)
+    if (!g.err && stream_error_word(s, &g.err) != LLMI_OK) return false;
     g.sk_grid = n_cu;
     return true;
 }
 }  // namespace
 
 bool gemm3_sk_attach(Gemm2Args& g, hipStream_t s) { return sk_setup(g, s); }
+
+int stream_errors(hipStream_t s, int* flags) {
+    LLMI_REQUIRE(flags, "stream_errors: flags must not be null");
+    *flags = 0;
+    int dev = 0;
+    LLMI_HIP(hipGetDevice(&dev));
+    int* e = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_ws_mu);
+        auto it = g_err.find({dev, s});
+        if (it != g_err.end()) e = it->second;
+    }
+    if (!e) return LLMI_OK;  // nothing on this stream could have set one
+    LLMI_HIP(hipMemcpyAsync(flags, e, sizeof(int), hipMemcpyDeviceToHost, s));
+    LLMI_HIP(hipMemsetAsync(e, 0, sizeof(int), s));
+    LLMI_HIP(hipStreamSynchronize(s));
+    return LLMI_OK;
+}
 
 bool linear_mfma_supported(int m, int n, int k) {
     return m >= 16 && k % 64 == 0 && gemm2_supported(n, k, EPI_STORE);

@@ -129,8 +129,8 @@ struct Gemm2Args {
     int bal_grid = 0;
     unsigned bal_epoch = 0;        // set by gemm3_launch
     int bal_own = 0;               // set by gemm3_launch: lo tile pairs each owner keeps
-    int* err = nullptr;
-    unsigned long long* stamps = nullptr;  // debug timeline of the balanced kernel (WgStamp), null = off            // sticky error word (bit 16: a lo partial never arrived)
+    int* err = nullptr;                    // sticky error word (bit 16: a lo / stream-K partial never arrived)
+    unsigned long long* stamps = nullptr;  // debug timeline of the balanced kernel (WgStamp), null = off
     // gemm3 stream-K (EPI_STORE / EPI_SILU_MUL with fewer 256 x 256 tiles than CUs; see
     // gemm3_sk_kernel): sk_grid workgroups (<= the CU count) share the tiles' K work evenly;
     // a tile's later pieces go to fp32 partial slots [tiles][sk_pmax][256 x 256] and set flags
@@ -151,6 +151,9 @@ Gemm3SkPlan gemm3_sk_plan(int m, int n, int k, int epi, int planes, int lo8, int
 // attach the stream-K workspace (per device and stream, gemm2.hip) to a gemm3 launch of g's
 // shape when the plan keeps <= 3 slots a tile; false: launch as before (LLMI_SK=0: never)
 bool gemm3_sk_attach(Gemm2Args& g, hipStream_t s);
+// reads and clears the sticky error bits that launches on s (this device) recorded when
+// their caller passed no error word (16: a stream-K partial never arrived); syncs s
+int stream_errors(hipStream_t s, int* flags);
 // bytes of the balanced gate_up's partial slots for m rows, n = 2 x intermediate (0: not used)
 size_t gemm3_bal_slab_bytes(int m, int n);
 // e4m3(W * 2^exp) of an fp16 [rows, cols] weight (exp chosen so that max |W| * 2^exp <= 448),

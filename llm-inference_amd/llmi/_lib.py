@@ -65,6 +65,7 @@ _SIGS = {
     "llmi_ffn": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _P]),
     "llmi_linear_residual": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P]),
     "llmi_ffn_residual": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P]),
+    "llmi_stream_errors": (_I, [_P, _P]),
     "llmi_batched_matmul": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_transpose_remove_pad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_synth_fill": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I, _P]),

@@ -7,6 +7,7 @@ through the C ABI on torch's current stream and raises on a non-zero status.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -315,6 +316,14 @@ def ffn_residual(x, w_gate_up, w_down, residual, gamma=None, eps: float = 1e-5, 
          gamma.data_ptr() if gamma is not None else None, _dt(gamma) if gamma is not None else 0, float(eps),
          _stream())
     return y
+
+
+def stream_errors() -> int:
+    """llmi_stream_errors: read and clear the device error bits recorded on the current stream
+    by the layer-API GEMM calls (16: a stream-K partial never arrived; synchronises)."""
+    flags = ctypes.c_int(0)
+    call("llmi_stream_errors", _stream(), ctypes.addressof(flags))
+    return flags.value
 
 
 def launchLinearStridedBatchGemm(input1, input2, trans_a: bool = False, trans_b: bool = False):

@@ -486,6 +486,9 @@ def test_ffn_stream_k_shape_matches_fp64(ops):
     e = rel(got, want)
     print(f"stream-K ffn m {m} hidden {hidden} inter {inter}: rel-L2 vs fp64 {e:.2e}")
     assert e < 1e-5
+    # every partial arrived: no sticky error bit on this stream, and reading clears it
+    assert ops.stream_errors() == 0
+    assert ops.stream_errors() == 0
 
 
 def test_ffn_without_stream_k_matches_fp64():
