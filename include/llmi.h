@@ -14,8 +14,10 @@
  *    thread-local message "[llmi][ERROR] ..." (the reference's LLM_CHECK text
  *    convention, src/utils/macro.h:113-133).
  *  - Row-major tensors. Linear weights are [out_features, in_features]
- *    (PyTorch nn.Linear layout; the reference calls cuBLAS with trans_b on
- *    exactly this layout, src/kernels/linear.cu:38-99).
+ *    (PyTorch nn.Linear layout; every layer of the reference calls cuBLAS with
+ *    trans_b on exactly this layout, src/kernels/linear.cu:38-99); the
+ *    launcher's other forms (weight [in, out], a transposed input) are
+ *    llmi_linear_trans.
  *  - Activations are fp32 unless a dtype argument says otherwise; weights
  *    may be fp32, fp16 or int8 (+ per-row fp16 scales, W8A16).
  *  - Nothing here blocks the host or allocates, except engine create/destroy and
@@ -88,6 +90,18 @@ int llmi_silu_mul(const float* gate_up, float* out, int n_tokens, int inter, llm
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m,
                 int n, int k, llmi_stream_t stream);
 
+/* launchLinearGemm (src/kernels/linear.h:16-22, linear.cu:38-99) with both of its flags,
+ * row-major: y[m, n] = op_a(x) . op_b(W), where
+ *   op_a(x) = x [m, k]            (trans_a = 0)  or  x^T with x stored [k, m]  (trans_a = 1),
+ *   op_b(W) = W stored [k, n]     (trans_b = 0, the reference's default: weight [in, out])
+ *          or W^T with W [n, k]   (trans_b = 1: nn.Linear's [out, in], llmi_linear).
+ * trans_b = 1, trans_a = 0 is llmi_linear itself; the other forms transpose the operand(s)
+ * into a per-(device, stream) scratch (grown outside stream capture: run the shape once
+ * before capturing) and then run llmi_linear, so every form has llmi_linear's arithmetic.
+ * f16 / f32 weights; int8 weights only with trans_b = 1 (their scales are per output row). */
+int llmi_linear_trans(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
+                      int trans_a, int trans_b, llmi_stream_t stream);
+
 /* LLaMAFFNLayer::forward (ffn.cpp:52-93) for context rows as one call: y [m, hidden] =
  * W_down (silu(W_gate x) * (W_up x)), x [m, hidden] fp32, w_gate_up [2 inter, hidden] (gate
  * rows then up rows, the reference's fused gate_up_proj) and w_down [hidden, inter] fp16.
@@ -120,6 +134,13 @@ int llmi_ffn_residual(const float* x, const void* w_gate_up, const void* w_down,
  * that output is incomplete. Synchronises the stream, stores the bits in *flags and clears
  * them. No counterpart in the reference (its cuBLAS calls have no cross-workgroup wait). */
 int llmi_stream_errors(llmi_stream_t stream, int* flags);
+
+/* Test hook for the stream-K hand-off (no reference counterpart): the next `launches`
+ * stream-K launches (any stream, this process) run with fault `mode` -- 1: no later piece
+ * ever publishes its flag (every owner waiting on one times out after 2 s and sets bit 16),
+ * 2: every later piece publishes 2.5 s late, after its owner gave up (a launch that follows
+ * must still be correct: flags carry a per-launch epoch). 0 / launches 0 clears it. */
+int llmi_debug_stream_k(int mode, int launches);
 
 /* One decode row through the HBM-streaming GEMV with its fused prologue/epilogue -- what
  * LlamaSelfDecoder::forward strings together for a token (self_decoder.cpp:59-81 fused):
@@ -306,6 +327,14 @@ int llmi_device_memset(void* ptr, int value, size_t bytes);
 int llmi_device_memset_async(void* ptr, int value, size_t bytes, llmi_stream_t stream);
 int llmi_memcpy(void* dst, const void* src, size_t bytes, int kind);
 int llmi_device_sync(void);
+
+/* Measured HBM read peak (the roofline's second denominator, SURVEY.md §8d timing rules):
+ * one-shot launches that each read `bytes` (rounded down to whole 32-KB pieces per
+ * workgroup) with non-temporal 16-B loads, 8 in flight per lane, cycling through the regions
+ * of a 2 GiB buffer so every launch streams from HBM (not the 256 MiB Infinity Cache), timed
+ * with HIP events over `iters` launches for grids of 512 / 1024 / 2048 / 4096 workgroups; the
+ * best grid's average microseconds per launch, its GB/s and the bytes one launch read. */
+int llmi_hbm_read_bench(size_t bytes, int iters, float* us, float* gbps, size_t* bytes_read);
 
 /* Synthetic prompt ids (bench config: 8 PRNG ids). Host only. */
 int llmi_synth_prompt(uint64_t seed, int n, int vocab, int32_t* out);

@@ -32,6 +32,25 @@ inline void* attn_workspace(int heads, int head_dim, int max_seq) {
 }
 inline int tokens_of(const Tensor* t) { return t->shape.size() >= 2 ? t->size() / t->shape.back() : 1; }
 
+// Device-side failures of launches with no error word of their own (the stream-K hand-off
+// in llmi_linear / llmi_ffn / the *_residual calls: bit 16 = a partial never arrived, the
+// output is incomplete) surface here as the reference's exception. The reference found its
+// errors at DeviceSyncAndCheckCudaError (macro.h:98-109) after each launch; the layer
+// classes call this once per forward. Synchronises the stream only when a launch on it
+// could have recorded a bit (llmi_stream_errors returns at once otherwise).
+inline void checkStreamErrors(void* stream, const char* who) {
+    int flags = 0;
+    LLMI_CALL(llmi_stream_errors(stream, &flags));
+    if (flags) {
+        std::ostringstream os;
+        os << "[oneLLM][ERROR] " << who << ": device error bits 0x" << std::hex << flags << std::dec
+           << ((flags & 16) ? " (a stream-K partial never arrived within 2 s -- another stream or process held "
+                              "CUs the launch needed -- so this forward's output is incomplete)"
+                            : "");
+        throw std::runtime_error(os.str());
+    }
+}
+
 // fp32 view of an activation tensor: TensorWrapper<float> as is; TensorWrapper<half_t>
 // converted into a device scratch buffer (load = copy the values in) and written back
 // rounded to fp16 by back(). The scratch is per (host thread, stream, slot): launchers
@@ -138,21 +157,30 @@ struct cublasWrapper {
     void* stream = nullptr;
 };
 
-// linear.h:16-22 -- output[m, n] = input[m, k] * weight[n, k]^T. The reference's
-// layers always pass trans_b = true for weights (masked_self_attention.cpp:62);
-// trans_a is not supported (it was unused on the decode path).
+// linear.h:16-22, linear.cu:38-99 -- output = op_a(input) . op_b(weight), row-major, with the
+// reference's defaults (trans_a = trans_b = false):
+//   trans_b = false: weight [k, n] (in, out) and op_b(W) = W      (linear.cu:60-66)
+//   trans_b = true:  weight [n, k] (out, in) and op_b(W) = W^T    (linear.cu:71-76; every
+//                    layer of the reference passes this, masked_self_attention.cpp:62)
+//   trans_a = false: input [m, k] (its trailing dims flattened: [tokens, heads, head])
+//   trans_a = true:  input [k, m] and op_a(x) = x^T               (linear.cu:78-84)
+// m = output->shape[0], as the reference's Cn (linear.cu:50). Every form runs llmi_linear's
+// arithmetic (the non-default ones transpose their operands first, llmi_linear_trans).
 template <typename AT, typename T>
 void launchLinearGemm(TensorWrapper<AT>* input, BaseWeight<T>& weight, TensorWrapper<AT>* output,
-                      cublasWrapper* cublas_wrapper = nullptr, bool trans_a = false, bool trans_b = true) {
-    LLM_CHECK_WITH_INFO(!trans_a, "launchLinearGemm: trans_a is not supported");
-    LLM_CHECK_WITH_INFO(trans_b, "launchLinearGemm: weights are [out, in] (trans_b = true)");
+                      cublasWrapper* cublas_wrapper = nullptr, bool trans_a = false, bool trans_b = false) {
     LLM_CHECK_WITH_INFO(weight.shape.size() == 2, "launchLinearGemm: weight must be 2-D");
-    const int k = weight.shape[1], n = weight.shape[0];
-    const int m = input->size() / k;
-    LLM_CHECK_WITH_INFO(m * k == input->size(), "launchLinearGemm: input size is not a multiple of in_features");
+    LLM_CHECK_WITH_INFO(input->shape.size() >= 2 && output->shape.size() >= 2,
+                        "launchLinearGemm: input and output must be at least 2-D");
+    const int k = trans_b ? weight.shape[1] : weight.shape[0], n = trans_b ? weight.shape[0] : weight.shape[1];
+    const int in_rows = input->shape[0], in_cols = input->size() / input->shape[0];
+    const int m = trans_a ? in_cols : in_rows;
+    LLM_CHECK_WITH_INFO((trans_a ? in_rows : in_cols) == k, "2nd dim of input MUST = 1st dim of weight");
+    LLM_CHECK_WITH_INFO(output->shape[0] == m && output->size() == m * n, "launchLinearGemm: output must be [m, n]");
     void* stream = cublas_wrapper ? cublas_wrapper->stream : nullptr;
     llmi_detail::Act<AT> in(input, 0, stream, true), out(output, 1, stream, false);
-    LLMI_CALL(llmi_linear(in.p, weight.data, llmiWeightDtype(getWeightType<T>()), weight.scale, out.p, m, n, k, stream));
+    LLMI_CALL(llmi_linear_trans(in.p, weight.data, llmiWeightDtype(getWeightType<T>()), weight.scale, out.p, m, n, k,
+                                trans_a ? 1 : 0, trans_b ? 1 : 0, stream));
     out.back(stream);
 }
 

@@ -279,6 +279,7 @@ public:
                            : LLMI_EUNSUPPORTED;
         if (rc == LLMI_OK) {
             out.store();
+            if (check_errors) llmi_detail::checkStreamErrors(stream, "LLaMAFFNLayer::forward");
             return;
         }
         if (rc != LLMI_EUNSUPPORTED) LLMI_CALL(rc);
@@ -286,7 +287,10 @@ public:
         launchAct(SwiGLU_input.get(), down_proj_input.get(), stream);
         launchLinearGemm(down_proj_input.get(), weights.down, out.get(), c, false, true);
         out.store();
+        if (check_errors) llmi_detail::checkStreamErrors(stream, "LLaMAFFNLayer::forward");
     }
+    // false: the caller (a decoder running many layers) checks once per forward instead
+    bool check_errors = true;
 
 private:
     int inter_size, hidden;
@@ -511,6 +515,7 @@ public:
                              out.get(), c, false, true);
             out.store();
             freeBuf();
+            if (check_errors) llmi_detail::checkStreamErrors(stream, "LLaMAContextAttentionLayer::forward");
             return;
         }
         // 1. qkv linear
@@ -557,7 +562,10 @@ public:
         launchLinearGemm(qkv_buf_wo_pad_1, weights.output, out.get(), c, false, true);
         out.store();
         freeBuf();
+        if (check_errors) llmi_detail::checkStreamErrors(stream, "LLaMAContextAttentionLayer::forward");
     }
+    // false: the caller (LlamaContextDecoder) checks once per forward instead
+    bool check_errors = true;
 
     // forward's steps 1-5 without o_proj, fused core only (fused(), after allocForForward):
     // qkv projection of x (fp32 [num_tokens, H]; for fp16 weights inside
@@ -645,7 +653,9 @@ public:
         : hidden_units(head_num * head_size), num_layer(num_layer), rmsnorm_eps(rmsnorm_eps), stream(stream),
           allocator(allocator),
           ctxAttn(head_num, kv_head_num, head_size, attn_params, stream, cublas_wrapper, allocator),
-          ffn(head_num, head_size, inter_size, stream, cublas_wrapper, allocator) {}
+          ffn(head_num, head_size, inter_size, stream, cublas_wrapper, allocator) {
+        ctxAttn.check_errors = ffn.check_errors = false;  // checked once at the end of forward
+    }
     ~LlamaContextDecoder() { freeBuf(); }
     // the attention core as one fused launch (default) or the reference's unfused chain
     void setFusedAttentionCore(bool on) { ctxAttn.setFusedCore(on); }
@@ -718,6 +728,9 @@ public:
         }
         dout.store();
         freeBuf();
+        // one check per forward, where the reference would have thrown at its next
+        // DeviceSyncAndCheckCudaError (context_attention.cpp:71-172)
+        llmi_detail::checkStreamErrors(stream, "LlamaContextDecoder::forward");
     }
 
 private:

@@ -1,6 +1,8 @@
 // extern "C" operator API (include/llmi.h): thin argument checks over the
 // kernels in gemv.hip / attn.hip / ops.hip. Never throws; errors are return
 // codes plus a thread-local message.
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "kernels.h"
@@ -106,6 +108,12 @@ int llmi_ffn_residual(const float* x, const void* w_gate_up, const void* w_down,
 
 int llmi_stream_errors(llmi_stream_t stream, int* flags) { return stream_errors(STREAM(stream), flags); }
 
+int llmi_debug_stream_k(int mode, int launches) {
+    LLMI_REQUIRE(mode >= 0 && mode <= 2 && launches >= 0, "debug_stream_k: mode 0..2, launches >= 0");
+    gemm3_sk_debug(mode, launches);
+    return LLMI_OK;
+}
+
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
                 llmi_stream_t stream) {
     LLMI_REQUIRE(m >= 1 && n >= 1 && k >= 1, "linear: m, n, k must be >= 1");
@@ -134,6 +142,65 @@ int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales
         LLMI_TRY(gemv_launch(a, STREAM(stream)));
     }
     return LLMI_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// llmi_linear_trans's operand scratch per (device, stream): [0] the transposed weight,
+// [1] the transposed input. Grown only outside stream capture, freed after a sync (earlier
+// launches on the stream may still read it).
+std::mutex g_tr_mu;
+std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> g_tr[2];
+int trans_scratch(int slot, hipStream_t s, size_t bytes, void** out) {
+    int dev = 0;
+    LLMI_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(g_tr_mu);
+    auto& e = g_tr[slot][{dev, s}];
+    if (bytes > e.second) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        LLMI_HIP(hipStreamIsCapturing(s, &cap));
+        LLMI_REQUIRE(cap == hipStreamCaptureStatusNone,
+                     "linear_trans: the transpose scratch must grow, which cannot happen while the stream is "
+                     "capturing (run the same shape once before capture)");
+        if (e.first) {
+            LLMI_HIP(hipStreamSynchronize(s));
+            LLMI_HIP(hipFree(e.first));
+            e = {nullptr, 0};
+        }
+        LLMI_HIP(hipMalloc(&e.first, bytes));
+        e.second = bytes;
+    }
+    *out = e.first;
+    return LLMI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int llmi_linear_trans(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
+                      int trans_a, int trans_b, llmi_stream_t stream) {
+    LLMI_REQUIRE(x && w && y && m >= 1 && n >= 1 && k >= 1, "linear_trans: null pointer or empty shape");
+    if (trans_b && !trans_a) return llmi_linear(x, w, w_dtype, w_scales, y, m, n, k, stream);
+    LLMI_REQUIRE(w_dtype == LLMI_F16 || w_dtype == LLMI_F32 || trans_b,
+                 "linear_trans: int8 weights are [out, in] with per-row scales (trans_b = 1 only)");
+    hipStream_t s = STREAM(stream);
+    const void* wt = w;
+    if (!trans_b) {  // W [k, n] -> [n, k]
+        void* buf = nullptr;
+        const int eb = w_dtype == LLMI_F16 ? 2 : 4;
+        LLMI_TRY(trans_scratch(0, s, (size_t)n * k * eb, &buf));
+        LLMI_TRY(transpose_launch(w, buf, k, n, eb, s));
+        wt = buf;
+    }
+    const float* xt = x;
+    if (trans_a) {  // x [k, m] -> [m, k]
+        void* buf = nullptr;
+        LLMI_TRY(trans_scratch(1, s, (size_t)m * k * sizeof(float), &buf));
+        LLMI_TRY(transpose_launch(x, buf, k, m, 4, s));
+        xt = static_cast<const float*>(buf);
+    }
+    return llmi_linear(xt, wt, w_dtype, w_scales, y, m, n, k, stream);
 }
 
 int llmi_linear_fused(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int n, int k,
@@ -356,6 +423,10 @@ int llmi_memcpy(void* dst, const void* src, size_t bytes, int kind) {
 int llmi_device_sync(void) {
     LLMI_HIP(hipDeviceSynchronize());
     return LLMI_OK;
+}
+
+int llmi_hbm_read_bench(size_t bytes, int iters, float* us, float* gbps, size_t* bytes_read) {
+    return hbm_read_bench(bytes, iters, us, gbps, bytes_read);
 }
 
 int llmi_synth_prompt(uint64_t seed, int n, int vocab, int32_t* out) {

@@ -808,7 +808,9 @@ struct Engine {
 
     // ------------------------------------------------ persistent ring layer (mode 1)
     bool ring_ok() const {
-        return wdt == LLMI_F16 && edt == LLMI_F16 && c.tp_world == 1 && !grouped &&
+        // layers >= 2: a launch zeroes the NEXT launch's counter block ((l + 1) % L), which for
+        // one layer would be its own, while its workgroups arrive on it
+        return wdt == LLMI_F16 && edt == LLMI_F16 && c.tp_world == 1 && !grouped && c.layers >= 2 &&
                ring_supported(c.hidden, hl, c.head_dim, il, ql + 2 * kvrows, n_cu);
     }
     int set_decode_mode(int mode) {
@@ -818,7 +820,7 @@ struct Engine {
             if (n_cu == 0) LLMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
             if (!ring_ok()) {
                 set_last_error("[llmi][ERROR] set_decode_mode: the ring layer needs fp16 weights, hidden 4096, "
-                               "head_dim 128, heads dividing the CU count, tp_world 1");
+                               "head_dim 128, heads dividing the CU count, tp_world 1, >= 2 layers");
                 return LLMI_EUNSUPPORTED;
             }
             int per_cu = 0;

@@ -565,10 +565,13 @@ int linear_workspace(hipStream_t s, size_t bytes, char** out) {
     return LLMI_OK;
 }
 int grid_of(size_t n4) { return (int)std::min<size_t>((n4 + kThreads - 1) / kThreads, 4096); }
-// gemm3 stream-K state per (device, stream): partial slots and their flags (zeroed when
-// allocated; every launch leaves them zero), grown like the linear workspace
+// gemm3 stream-K state per (device, stream): partial slots, and the control words (epoch,
+// finished count: 256 B) followed by the flags, all zeroed when allocated; grown like the
+// linear workspace
 std::map<std::pair<int, hipStream_t>, std::pair<std::pair<void*, size_t>, std::pair<unsigned*, size_t>>> g_sk;
-int sk_workspace(hipStream_t s, size_t slab_bytes, size_t flag_bytes, float** slab, unsigned** flags) {
+constexpr size_t kSkCtlBytes = kSkCtlWords * sizeof(unsigned);
+int sk_workspace(hipStream_t s, size_t slab_bytes, size_t flag_bytes, float** slab, unsigned** flags, unsigned** ctl) {
+    flag_bytes += kSkCtlBytes;
     int dev = 0;
     LLMI_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(g_ws_mu);
@@ -591,7 +594,8 @@ int sk_workspace(hipStream_t s, size_t slab_bytes, size_t flag_bytes, float** sl
         e.second.second = fb;
     }
     *slab = static_cast<float*>(e.first.first);
-    *flags = e.second.first;
+    *ctl = e.second.first;
+    *flags = e.second.first + kSkCtlBytes / sizeof(unsigned);
     return LLMI_OK;
 }
 // sticky device error bits per (device, stream) for launches whose caller passes no error
@@ -632,7 +636,7 @@ bool sk_setup(Gemm2Args& g, hipStream_t s) {
     const int n_cu = cu_count();
     const Gemm3SkPlan p = gemm3_sk_plan(g.m, g.n, g.k, g.epi, g.planes, g.lo8, n_cu);
     if (p.pmax < 1 || p.pmax > 3) return false;
-    if (sk_workspace(s, p.slab_bytes, p.flag_bytes, &g.sk_slab, &g.sk_flags) != LLMI_OK) return false;
+    if (sk_workspace(s, p.slab_bytes, p.flag_bytes, &g.sk_slab, &g.sk_flags, &g.sk_ctl) != LLMI_OK) return false;
     // a partial that never arrives sets bit 16 somewhere the caller can read (stream_errors)
     if (!g.err && stream_error_word(s, &g.err) != LLMI_OK) return false;
     g.sk_grid = n_cu;
@@ -704,7 +708,7 @@ int linear_mfma_launch(const float* x, const void* w, float* y, int m, int n, in
     Gemm2Args g;
     g.a[0] = hi; g.a[1] = lo; g.planes = 2; g.lda = k;
     g.w = w; g.m = m; g.n = n; g.k = k; g.ldy = n;
-    if (sk) { g.sk_slab = skg.sk_slab; g.sk_flags = skg.sk_flags; g.sk_grid = skg.sk_grid; }
+    if (sk) { g.sk_slab = skg.sk_slab; g.sk_flags = skg.sk_flags; g.sk_ctl = skg.sk_ctl; g.sk_grid = skg.sk_grid; g.err = skg.err; }
     float* sl = reinterpret_cast<float*>(ws + 2 * plane);
     if (ks > 1) {
         g.epi = EPI_SLAB; g.ksplit = ks; g.slab = sl; g.y = re || raw ? sl : y;

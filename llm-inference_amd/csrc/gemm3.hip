@@ -518,10 +518,14 @@ __global__ __launch_bounds__(kT) void gemm3_silu_bal_kernel(Gemm2Args a) {
 // contiguous ranges, one per workgroup, that cross tile boundaries. The workgroup holding a
 // tile's first pair owns it: that is the END of its range, so the tile's later pieces (the
 // START of the next workgroups' ranges) were computed first and the owner's wait is short.
-// Later pieces go to fp32 partial slots and set a flag; the owner waits for the flags
-// (bounded: error bit 16), resets them (a graph replay finds them zero), adds the slots in
-// order onto its own piece (repeatable sums) and runs the tile's epilogue. Every workgroup
-// is resident (sk_grid <= the CU count, one 136-KB workgroup per CU), so waits always end.
+// Later pieces go to fp32 partial slots and raise a flag to the launch's epoch E; the owner
+// waits for flag == E (bounded: error bit 16), adds the slots in order onto its own piece
+// (repeatable sums) and runs the tile's epilogue. Flags are never reset: a piece that
+// publishes after its owner timed out leaves E behind, which no later launch waits for.
+// E = the last completed launch's epoch + 1, read from sk_ctl[0]; the last workgroup to
+// finish (a count in sk_ctl[32]) stores E there, so eager launches and graph replays alike
+// see a new value each launch. Every workgroup is resident (sk_grid <= the CU count, one
+// 136-KB workgroup per CU), so waits end unless another stream or process holds CUs.
 #ifndef LLMI_SK_EXP
 #define LLMI_SK_EXP 0  // timing-only builds: 1 = flags without the slot payload, 2 = no hand-off at all
 #endif
@@ -555,11 +559,18 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
     const int MT = d.m_tiles, Gp = G / MT, v = w / MT, rt = w % MT;
     const long TPs = (long)a.n_tiles * d.U2;  // pairs of all column stripes
     const long p1 = (long)(v + 1) * TPs / Gp;
+    unsigned* const ctl = a.sk_flags - kSkCtlWords;  // the control words sit just before the flags
+    const int pmax = a.sk_pmax & 255, sk_test = a.sk_pmax >> 8;
     auto slot_rsrc = [&](int tile, int slot) {  // one 256 KB partial slot (wave-uniform)
-        return __builtin_amdgcn_make_buffer_rsrc(a.sk_slab + ((size_t)tile * a.sk_pmax + slot) * kTile * kTile, (short)0,
+        return __builtin_amdgcn_make_buffer_rsrc(a.sk_slab + ((size_t)tile * pmax + slot) * kTile * kTile, (short)0,
                                                  kTile * kTile * 4, 0x00020000);
     };
     __shared__ int ok_s[8];
+    // this launch's epoch (thread 0 only: it alone publishes and waits; 0 is never used)
+    auto epoch = [&]() {
+        const unsigned e = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        return e ? e : 1u;
+    };
     // a range shorter than a tile (T < G) meets at most two tiles: the piece (seg) of each
     auto seg = [&](long p) {
         f4v acc[2][2][4][2];
@@ -589,19 +600,26 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
                                                                    (((x * 2 + y) * 4 + i) * 2 + j) * kT * 16, 16);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, then one flag
             __syncthreads();
-            if (t == 0 && LLMI_SK_EXP != 2)
-                __hip_atomic_store(a.sk_flags + tile * a.sk_pmax + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0 && LLMI_SK_EXP != 2 && sk_test != 1) {
+                if (sk_test == 2) {  // fault injection: publish after the owner's 2-s bound
+                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__builtin_amdgcn_s_memrealtime() - t0 < 250000000ull) __builtin_amdgcn_s_sleep(127);
+                }
+                __hip_atomic_store(a.sk_flags + tile * pmax + sl, epoch(), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else {
             zero_acc(acc);
             g3_run<EPI>(a, lds, m0, ct, 0, nhi, lo0, nlo, acc);  // a tile's head: from K tile 0
             const int np = LLMI_SK_EXP == 2 ? 0 : sk_wg_of((long)ct * d.U2 + d.U2 - 1, TPs, Gp) - v;  // later pieces
             if (np > 0) {
                 if (t == 0) {
+                    const unsigned E = epoch();
                     for (int sl = 0; sl < np; ++sl) {
-                        unsigned* f = a.sk_flags + tile * a.sk_pmax + sl;
+                        unsigned* f = a.sk_flags + tile * pmax + sl;
                         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                         int ok = 1;
-                        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != E) {
                             __builtin_amdgcn_s_sleep(2);
                             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
                                 if (a.err) atomicOr(a.err, 16);
@@ -610,7 +628,6 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
                             }
                         }
                         ok_s[sl] = ok;
-                        __hip_atomic_store(f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one L2 invalidate, then the barrier
                 }
@@ -639,11 +656,23 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
         }
         return (long)ct * d.U2 + e;
     };
-    if (v >= Gp) return;  // G not a multiple of m_tiles: the spare workgroups
-    const long p0 = (long)v * TPs / Gp;
-    if (p0 >= p1) return;
-    const long pn = seg(p0);
-    if (pn < p1) seg(pn);
+    if (v < Gp) {  // G not a multiple of m_tiles: the spare workgroups only count themselves
+        const long p0 = (long)v * TPs / Gp;
+        if (p0 < p1) {
+            const long pn = seg(p0);
+            if (pn < p1) seg(pn);
+        }
+    }
+    // every workgroup read the epoch (if at all) before counting itself here, so the last
+    // one can advance it for the next launch
+    if (t == 0) {
+        const unsigned done = __hip_atomic_fetch_add(ctl + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == (unsigned)G - 1u) {
+            const unsigned E = epoch();
+            __hip_atomic_store(ctl + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 template <int EPI>
@@ -739,6 +768,14 @@ size_t gemm3_bal_slab_bytes(int m, int n) {
     return tiles * 2 * kTile * kTile * sizeof(float);
 }
 
+namespace {
+std::atomic<int> g_sk_debug_mode{0}, g_sk_debug_left{0};
+}
+void gemm3_sk_debug(int mode, int launches) {
+    g_sk_debug_mode = mode;
+    g_sk_debug_left = mode ? launches : 0;
+}
+
 Gemm3SkPlan gemm3_sk_plan(int m, int n, int k, int epi, int planes, int lo8, int g) {
     Gemm3SkPlan p;
     if ((epi != EPI_STORE && epi != EPI_SILU_MUL) || m <= 0 || g <= 0 || !gemm3_supported(n, k, epi, 1)) return p;
@@ -827,7 +864,12 @@ int gemm3_launch(Gemm2Args a, hipStream_t s) {
     if (a.sk_slab && a.sk_flags && a.sk_grid > 0 && (a.epi == EPI_STORE || a.epi == EPI_SILU_MUL)) {
         const Gemm3SkPlan p = gemm3_sk_plan(a.m, a.n, a.k, a.epi, a.planes, a.lo8, a.sk_grid);
         LLMI_REQUIRE(p.pmax > 0, "gemm3: stream-K requested for a shape it does not cover (see gemm3_sk_plan)");
-        a.sk_pmax = p.pmax;
+        LLMI_REQUIRE(a.sk_ctl && a.sk_ctl + kSkCtlWords == a.sk_flags,
+                     "gemm3: stream-K needs its control words just before the flags (sk_workspace)");
+        int left = g_sk_debug_left.load();
+        while (left > 0 && !g_sk_debug_left.compare_exchange_weak(left, left - 1)) {
+        }
+        a.sk_pmax = p.pmax | ((left > 0 ? g_sk_debug_mode.load() : 0) << 8);  // + the fault-injection mode
         if (a.epi == EPI_STORE) return launch_sk<EPI_STORE>(a, s);
         return launch_sk<EPI_SILU_MUL>(a, s);
     }

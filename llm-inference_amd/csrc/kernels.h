@@ -133,13 +133,21 @@ struct Gemm2Args {
     unsigned long long* stamps = nullptr;  // debug timeline of the balanced kernel (WgStamp), null = off
     // gemm3 stream-K (EPI_STORE / EPI_SILU_MUL with fewer 256 x 256 tiles than CUs; see
     // gemm3_sk_kernel): sk_grid workgroups (<= the CU count) share the tiles' K work evenly;
-    // a tile's later pieces go to fp32 partial slots [tiles][sk_pmax][256 x 256] and set flags
-    // [tiles][sk_pmax] (zeroed once; the tile's first workgroup resets each after reading)
+    // a tile's later pieces go to fp32 partial slots [tiles][sk_pmax][256 x 256] and raise flags
+    // [tiles][sk_pmax] to the launch's epoch (zeroed once, never reset: a piece that publishes
+    // after its owner gave up cannot satisfy a later launch's wait). sk_ctl: [0] the epoch of
+    // the last completed launch, [32] the launch's finished-workgroup count (the last one
+    // advances [0] and re-zeroes [32]), so graph replays get fresh epochs too.
     float* sk_slab = nullptr;
     unsigned* sk_flags = nullptr;
+    unsigned* sk_ctl = nullptr;    // = sk_flags - kSkCtlWords (the kernel derives it from sk_flags)
     int sk_grid = 0;
-    int sk_pmax = 0;
+    int sk_pmax = 0;               // set by gemm3_launch; bits 8+: fault injection (llmi_debug_stream_k:
+                                   // 1 never publish, 2 publish 2.5 s late)
 };
+constexpr int kSkCtlWords = 64;    // stream-K control words ahead of the flags (256 B)
+// the next `launches` stream-K launches run with sk_test = mode (llmi_debug_stream_k)
+void gemm3_sk_debug(int mode, int launches);
 // stream-K plan for gemm3 (m rows, n columns -- gate_up: 2 x inter --, k, planes / lo8 as in
 // Gemm2Args) on g workgroups: slots per tile (0: stream-K does not apply), and the bytes of
 // partial slots and of flags it needs
@@ -420,6 +428,10 @@ int xchg_launch(const XchgArgs& a, hipStream_t s);
 // ---------------------------------------------------------- synthetic
 // in-place reduction over W rank buffers (device array of pointers); op 0 i64 sum, 1 f32 sum, 2 u64 max
 int convert_launch(const void* src, int src_dtype, void* dst, int dst_dtype, size_t n, hipStream_t s);
+// measured HBM read peak (llmi_hbm_read_bench, include/llmi.h)
+int hbm_read_bench(size_t bytes, int iters, float* us, float* gbps, size_t* bytes_read);
+// src [rows][cols] -> dst [cols][rows] for 2- or 4-byte elements (raw bits)
+int transpose_launch(const void* src, void* dst, int rows, int cols, int elem_bytes, hipStream_t s);
 int group_reduce_launch(void* const* dev_bufs, int W, int n, int op, hipStream_t s);
 int synth_fill_launch(void* out, int out_dtype, int kind, uint64_t seed, uint32_t tid, int rows,
                       int cols, int row0, int col0, int ld, hipStream_t s);

@@ -303,6 +303,109 @@ __global__ void convert_kernel(const void* src, int sdt, void* dst, int ddt, siz
     }
 }
 
+// src [rows][cols] -> dst [cols][rows], elements moved as raw bits (fp16 / fp32), 64 x 64
+// tiles through LDS so both the reads and the writes run along rows
+template <typename E>
+__global__ __launch_bounds__(256) void transpose_kernel(const E* src, E* dst, int rows, int cols) {
+    __shared__ E t[64][65];
+    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int r = i / 64, c = i % 64;
+        if (r0 + r < rows && c0 + c < cols) t[r][c] = src[(size_t)(r0 + r) * cols + c0 + c];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int c = i / 64, r = i % 64;
+        if (r0 + r < rows && c0 + c < cols) dst[(size_t)(c0 + c) * rows + r0 + r] = t[r][c];
+    }
+}
+
+int transpose_launch(const void* src, void* dst, int rows, int cols, int elem_bytes, hipStream_t s) {
+    LLMI_REQUIRE(src && dst && src != dst && rows > 0 && cols > 0 && (elem_bytes == 2 || elem_bytes == 4),
+                 "transpose: bad arguments (distinct buffers, 2- or 4-byte elements)");
+    LLMI_REQUIRE((rows + 63) / 64 <= 65535, "transpose: too many row tiles");
+    const dim3 g((cols + 63) / 64, (rows + 63) / 64);
+    if (elem_bytes == 2)
+        hipLaunchKernelGGL(transpose_kernel<uint16_t>, g, dim3(256), 0, s, static_cast<const uint16_t*>(src),
+                           static_cast<uint16_t*>(dst), rows, cols);
+    else
+        hipLaunchKernelGGL(transpose_kernel<uint32_t>, g, dim3(256), 0, s, static_cast<const uint32_t*>(src),
+                           static_cast<uint32_t*>(dst), rows, cols);
+    LLMI_HIP(hipGetLastError());
+    return LLMI_OK;
+}
+
+// HBM read microbench (hbm_read_bench): workgroup g reads its contiguous `per` bytes in
+// rounds of 8 non-temporal 16-B loads per lane (32 KB a round), all issued before any use
+__global__ __launch_bounds__(256) void hbm_read_kernel(const char* base, size_t per, unsigned* sink) {
+    const char* p = base + (size_t)blockIdx.x * per + threadIdx.x * 16;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    unsigned acc = 0;
+    for (size_t off = 0; off < per; off += 8 * 4096) {
+        u32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + off + i * 4096));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+    }
+    if (acc == 0x9e3779b9u) sink[blockIdx.x] = acc;  // never taken for the memset pattern; keeps the loads
+}
+
+int hbm_read_bench(size_t bytes, int iters, float* us_out, float* gbps_out, size_t* read_out) {
+    LLMI_REQUIRE(us_out && gbps_out && read_out && iters > 0 && bytes >= ((size_t)1 << 20) &&
+                     bytes <= ((size_t)1 << 30),
+                 "hbm_read_bench: 1 MiB <= bytes <= 1 GiB, iters > 0");
+    const size_t cap = (size_t)2 << 30;
+    char* buf = nullptr;
+    unsigned* sink = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    LLMI_HIP(hipMalloc(&buf, cap));
+    int rc = LLMI_OK;
+    float best_us = 0.f;
+    size_t best_bytes = 0;
+    if (hipMalloc(&sink, 4096 * sizeof(unsigned)) != hipSuccess || hipMemset(buf, 0x5a, cap) != hipSuccess ||
+        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+        rc = LLMI_EHIP;
+    } else {
+        for (int grid : {512, 1024, 2048, 4096}) {
+            const size_t per = bytes / grid / 32768 * 32768;
+            if (per == 0) continue;
+            const size_t total = per * grid;
+            const size_t region = (total + ((size_t)2 << 20) - 1) / ((size_t)2 << 20) * ((size_t)2 << 20);
+            const int nreg = (int)(cap / region);
+            for (int i = 0; i < 3; ++i)
+                hipLaunchKernelGGL(hbm_read_kernel, dim3(grid), dim3(256), 0, nullptr, buf + (size_t)(i % nreg) * region, per, sink);
+            (void)hipEventRecord(e0, nullptr);
+            for (int i = 0; i < iters; ++i)
+                hipLaunchKernelGGL(hbm_read_kernel, dim3(grid), dim3(256), 0, nullptr,
+                                   buf + (size_t)((i + 3) % nreg) * region, per, sink);
+            (void)hipEventRecord(e1, nullptr);
+            float ms = 0.f;
+            if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+                rc = LLMI_EHIP;
+                break;
+            }
+            const float us = ms * 1000.f / iters;
+            if (best_bytes == 0 || total / us > best_bytes / best_us) {
+                best_us = us;
+                best_bytes = total;
+            }
+        }
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (sink) (void)hipFree(sink);
+    (void)hipFree(buf);
+    if (rc != LLMI_OK) {
+        set_last_error("[llmi][ERROR] hbm_read_bench: a HIP call failed");
+        return rc;
+    }
+    *us_out = best_us;
+    *gbps_out = best_bytes / (best_us * 1e-6f) / 1e9f;
+    *read_out = best_bytes;
+    return LLMI_OK;
+}
+
 int convert_launch(const void* src, int src_dtype, void* dst, int dst_dtype, size_t n, hipStream_t s) {
     LLMI_REQUIRE((src_dtype == LLMI_F16 || src_dtype == LLMI_F32) && (dst_dtype == LLMI_F16 || dst_dtype == LLMI_F32),
                  "convert: dtypes must be f16 or f32");

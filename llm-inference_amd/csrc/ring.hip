@@ -620,21 +620,6 @@ __global__ __launch_bounds__(kThreads, 1) void ring_layer_kernel(RingArgs a) {
     prof_out();
 }
 
-// W [rows][cols] -> W^T [cols][rows], fp16, 64 x 64 tiles through LDS
-__global__ __launch_bounds__(256) void transpose_f16_kernel(const __half* src, __half* dst, int rows, int cols) {
-    __shared__ __half t[64][66];
-    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int r = i / 64, c = i % 64;
-        if (r0 + r < rows && c0 + c < cols) t[r][c] = src[(size_t)(r0 + r) * cols + c0 + c];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int c = i / 64, r = i % 64;
-        if (r0 + r < rows && c0 + c < cols) dst[(size_t)(c0 + c) * rows + r0 + r] = t[r][c];
-    }
-}
-
 }  // namespace
 
 bool ring_supported(int hidden, int heads, int head_dim, int inter, int n_qkv, int n_cu) {
@@ -674,12 +659,7 @@ int ring_residency(int* per_cu) {
 }
 
 int transpose_f16_launch(const void* src, void* dst, int rows, int cols, hipStream_t s) {
-    LLMI_REQUIRE(src && dst && rows > 0 && cols > 0, "transpose_f16: bad arguments");
-    const dim3 g((cols + 63) / 64, (rows + 63) / 64);
-    hipLaunchKernelGGL(transpose_f16_kernel, g, dim3(256), 0, s, reinterpret_cast<const __half*>(src),
-                       reinterpret_cast<__half*>(dst), rows, cols);
-    LLMI_HIP(hipGetLastError());
-    return LLMI_OK;
+    return transpose_launch(src, dst, rows, cols, 2, s);
 }
 
 }  // namespace llmi

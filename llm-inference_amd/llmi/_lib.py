@@ -44,6 +44,7 @@ _SIGS = {
     "llmi_silu_mul": (_I, [_P, _P, _I, _I, _P]),
     "llmi_convert": (_I, [_P, _I, _P, _I, _SZ, _P]),
     "llmi_linear": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _P]),
+    "llmi_linear_trans": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "llmi_linear_fused": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _I, _F, _I, _P, _P]),
     "llmi_rope_decode": (_I, [_P, _I, _I, _I, _I, _F, _P]),
     "llmi_attn_workspace_bytes": (_SZ, [_I, _I, _I]),
@@ -66,6 +67,8 @@ _SIGS = {
     "llmi_linear_residual": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P]),
     "llmi_ffn_residual": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P]),
     "llmi_stream_errors": (_I, [_P, _P]),
+    "llmi_debug_stream_k": (_I, [_I, _I]),
+    "llmi_hbm_read_bench": (_I, [_SZ, _I, _P, _P, _P]),
     "llmi_batched_matmul": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_transpose_remove_pad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_synth_fill": (_I, [_P, _I, _I, _U64, _U32, _I, _I, _I, _I, _I, _P]),

@@ -79,13 +79,21 @@ def launchAct(gate_up: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def launchLinearGemm(x: torch.Tensor, w: torch.Tensor, scales: torch.Tensor = None) -> torch.Tensor:
-    """y = x @ w^T (trans_b = true); w [n, k] f32/f16/i8 (+ per-row f16 scales for i8)."""
+def launchLinearGemm(x: torch.Tensor, w: torch.Tensor, scales: torch.Tensor = None, trans_a: bool = False,
+                     trans_b: bool = True) -> torch.Tensor:
+    """y = op_a(x) @ op_b(w) (llmi_linear_trans; linear.cu:38-99). This Python mirror keeps
+    torch's nn.Linear layout as its default (trans_b = True: w [n, k], y = x @ w^T); the C++
+    mirror (include/llmi/kernels.h) keeps the reference's defaults (trans_a = trans_b = false).
+    trans_b False: w [k, n], y = x @ w; trans_a True: x [k, m], y = x^T @ op_b(w).
+    w f32/f16, or i8 (+ per-row f16 scales) with trans_b only."""
     _dev(x, w)
-    m, k = x.shape
-    n = w.shape[0]
+    m, k = (x.shape[1], x.shape[0]) if trans_a else x.shape
+    n = w.shape[0] if trans_b else w.shape[1]
+    if (w.shape[1] if trans_b else w.shape[0]) != k:
+        raise ValueError(f"launchLinearGemm: x gives k = {k}, w has shape {tuple(w.shape)} (trans_b={trans_b})")
     y = torch.empty(m, n, device=x.device, dtype=torch.float32)
-    call("llmi_linear", x.data_ptr(), w.data_ptr(), _dt(w), _p(scales), y.data_ptr(), m, n, k, _stream())
+    call("llmi_linear_trans", x.contiguous().data_ptr(), w.contiguous().data_ptr(), _dt(w), _p(scales), y.data_ptr(),
+         m, n, k, int(trans_a), int(trans_b), _stream())
     return y
 
 
@@ -278,23 +286,38 @@ def context_attention_proj(x, w_qkv, padding_offset, history_length, input_lengt
     return out
 
 
-def ffn(x, w_gate_up, w_down):
+def check_stream(what: str) -> None:
+    """Raise LlmiError when a launch on the current stream recorded a device error bit
+    (llmi_stream_errors; 16 = a stream-K partial never arrived, the output is incomplete) --
+    the reference's DeviceSyncAndCheckCudaError (macro.h:98-109). Synchronises the stream
+    only when a launch on it could have recorded one."""
+    f = stream_errors()
+    if f:
+        why = " (a stream-K partial never arrived within 2 s: the output is incomplete)" if f & 16 else ""
+        raise _lib.LlmiError(f"{what}: device error bits {f:#x}{why}")
+
+
+def ffn(x, w_gate_up, w_down, check: bool = True):
     """LLaMAFFNLayer for context rows in one call (llmi_ffn): x [m, hidden] fp32, w_gate_up
     [2 inter, hidden] and w_down [hidden, inter] fp16 -> [m, hidden] fp32. Raises
-    LlmiError (unsupported) where the fused form does not apply."""
+    LlmiError (unsupported) where the fused form does not apply, and (check) when the
+    stream-K hand-off failed (check_stream; False leaves that to the caller, e.g. once per
+    forward of many layers)."""
     _dev(x, w_gate_up, w_down)
     m, hidden = x.shape
     inter = w_down.shape[1]
     y = torch.empty(m, hidden, device=x.device, dtype=torch.float32)
     call("llmi_ffn", x.contiguous().data_ptr(), w_gate_up.data_ptr(), w_down.data_ptr(), _dt(w_gate_up), y.data_ptr(),
          m, hidden, inter, _stream())
+    if check:
+        check_stream("llmi_ffn")
     return y
 
 
-def linear_residual(x, w, residual, gamma=None, eps: float = 1e-5, out: bool = True):
+def linear_residual(x, w, residual, gamma=None, eps: float = 1e-5, out: bool = True, check: bool = True):
     """llmi_linear_residual: residual += x . w^T (in place), then returns RMSNorm(residual) *
     gamma (gamma None: a copy of the residual; out False: None). x [m, k] fp32, w [n, k] fp16,
-    residual [m, n] fp32, gamma [n] fp16 / fp32."""
+    residual [m, n] fp32, gamma [n] fp16 / fp32. check: as ffn."""
     _dev(x, w, residual)
     m, k = x.shape
     n = w.shape[0]
@@ -302,10 +325,13 @@ def linear_residual(x, w, residual, gamma=None, eps: float = 1e-5, out: bool = T
     call("llmi_linear_residual", x.contiguous().data_ptr(), w.data_ptr(), _dt(w), m, n, k, residual.data_ptr(),
          y.data_ptr() if out else None, gamma.data_ptr() if gamma is not None else None,
          _dt(gamma) if gamma is not None else 0, float(eps), _stream())
+    if check:
+        check_stream("llmi_linear_residual")
     return y
 
 
-def ffn_residual(x, w_gate_up, w_down, residual, gamma=None, eps: float = 1e-5, out: bool = True):
+def ffn_residual(x, w_gate_up, w_down, residual, gamma=None, eps: float = 1e-5, out: bool = True,
+                 check: bool = True):
     """llmi_ffn_residual: residual += FFN(x) (in place), then the output as linear_residual."""
     _dev(x, w_gate_up, w_down, residual)
     m, hidden = x.shape
@@ -315,7 +341,15 @@ def ffn_residual(x, w_gate_up, w_down, residual, gamma=None, eps: float = 1e-5, 
          hidden, inter, residual.data_ptr(), y.data_ptr() if out else None,
          gamma.data_ptr() if gamma is not None else None, _dt(gamma) if gamma is not None else 0, float(eps),
          _stream())
+    if check:
+        check_stream("llmi_ffn_residual")
     return y
+
+
+def debug_stream_k(mode: int, launches: int = 1) -> None:
+    """llmi_debug_stream_k (test hook): the next `launches` stream-K launches never publish a
+    later piece (mode 1) or publish it 2.5 s late (mode 2); mode 0 clears."""
+    call("llmi_debug_stream_k", int(mode), int(launches))
 
 
 def stream_errors() -> int:

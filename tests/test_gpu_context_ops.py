@@ -491,6 +491,48 @@ def test_ffn_stream_k_shape_matches_fp64(ops):
     assert ops.stream_errors() == 0
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_ffn_stream_k_fault_raises_and_next_call_is_clean(ops, mode):
+    """A stream-K piece that never publishes (mode 1) or publishes 2.5 s late, after its owner
+    gave up (mode 2; the late flag must not satisfy a later launch's wait): llmi_ffn's result
+    is flagged (bit 16) and ops.ffn raises; the next call is bitwise the clean result."""
+    from llmi._lib import LlmiError
+    rng = np.random.default_rng(32)
+    m, hidden, inter = 512, 1024, 6144
+    x = rng.standard_normal((m, hidden)).astype(np.float32)
+    wgu = (rng.standard_normal((2 * inter, hidden)) / math.sqrt(hidden)).astype(np.float16)
+    wd = (rng.standard_normal((hidden, inter)) / math.sqrt(inter)).astype(np.float16)
+    tx, tgu, td = T(x), T(wgu), T(wd)
+    clean = N(ops.ffn(tx, tgu, td))
+    ops.debug_stream_k(mode, 1)
+    try:
+        with pytest.raises(LlmiError, match="stream-K partial never arrived"):
+            ops.ffn(tx, tgu, td)
+    finally:
+        ops.debug_stream_k(0, 0)
+    assert ops.stream_errors() == 0  # read and cleared by the raise
+    np.testing.assert_array_equal(N(ops.ffn(tx, tgu, td)), clean)
+    np.testing.assert_array_equal(N(ops.ffn(tx, tgu, td)), clean)
+
+
+@pytest.mark.parametrize("trans_a,trans_b", [(False, False), (True, False), (True, True), (False, True)])
+@pytest.mark.parametrize("m", [3, 32])
+def test_linear_trans_forms_match_fp64(ops, trans_a, trans_b, m):
+    """launchLinearGemm (llmi_linear_trans) in every (trans_a, trans_b) form of linear.cu:38-99
+    on a non-square, non-symmetric fp16 weight: against float64 within 1e-6 (rel-L2)."""
+    rng = np.random.default_rng(40 + m)
+    k, n = 1024, 1536
+    x = rng.standard_normal((m, k)).astype(np.float32)
+    w = (rng.standard_normal((n, k)) / math.sqrt(k)).astype(np.float16)  # [out, in]
+    xa = x.T.copy() if trans_a else x
+    wb = w if trans_b else w.T.copy()
+    got = N(ops.launchLinearGemm(T(xa), T(wb), trans_a=trans_a, trans_b=trans_b))
+    want = x.astype(np.float64) @ w.astype(np.float64).T
+    e = rel(got, want)
+    print(f"linear m {m} trans_a {trans_a} trans_b {trans_b}: rel-L2 vs fp64 {e:.2e}")
+    assert got.shape == (m, n) and e < 1e-6
+
+
 def test_ffn_without_stream_k_matches_fp64():
     """LLMI_SK=0 (the knob that turns gemm3 stream-K off) in a child process: llmi_ffn at the
     stream-K shape on the plain 172-tile launch, against float64 within the same 1e-5."""

@@ -174,3 +174,14 @@ def test_ring_timing_restores_state():
             outs.append((e.tokens(), e.logits().copy()))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def test_ring_refuses_one_layer_models():
+    """A ring launch zeroes the next launch's counter block ((l + 1) % L); with one layer that
+    is its own block, so mode 1 is refused for L = 1 (unsupported, nothing changes)."""
+    cfg = preset("llama2-7b", layers=1, max_seq=64)
+    with Engine(cfg) as e:
+        e.load_synthetic(1)
+        with pytest.raises(_lib.LlmiError, match=">= 2 layers"):
+            e.set_decode_mode(1)
+        e.set_decode_mode(0)
