@@ -479,6 +479,16 @@ int llmi_engine_set_decode_mode(llmi_engine* e, int mode);
  * A peer that never arrives (2 s) sets error bit 8: llmi_engine_tokens fails, no hang. */
 int llmi_engine_xchg_handle(llmi_engine* e, void* out64);
 int llmi_engine_xchg_open(llmi_engine* e, const void* handles);
+
+/* One-GPU pricing of ONE tensor-parallel rank (no reference counterpart): a tp_world > 1
+ * engine without peers runs its shard's whole token loop with every peer inbox replaced by
+ * its own -- the push writes this rank's slice into its own slot and zeros into the W - 1
+ * others (the same bytes a real push writes), raises all W flags, and the reduce sums to
+ * this rank's own partial. Tokens are NOT the TP model's (the other ranks' partials are
+ * zero); the launch / exchange structure and its timing are. set_exchange 0 then runs no
+ * exchange at all (the compute-only floor), 1 the one-shot exchange launches, 2 the
+ * exchange fused into the producers. */
+int llmi_engine_xchg_loopback(llmi_engine* e);
 int llmi_engine_set_exchange(llmi_engine* e, int mode);
 /* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built
  * afterwards) write a per-workgroup timeline into dev_buf (8 x uint64 per

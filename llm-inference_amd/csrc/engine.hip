@@ -766,6 +766,7 @@ struct Engine {
         a.mode = mode;
         a.cap_n = xchg_cap_n;
         a.cap_w = c.tp_world;
+        a.loop = xchg_loop;
         return a;
     }
     int exchange(void* buf, int n, int op) {
@@ -789,6 +790,7 @@ struct Engine {
         return LLMI_OK;
     }
     bool peers_ready = false;
+    int xchg_loop = 0;  // llmi_engine_xchg_loopback: one rank alone, every peer its own inbox
 
     int set_sampling(int k, uint64_t sd) {
         LLMI_REQUIRE(k >= 0 && k <= 16, "set_sampling: k must be in [0, 16] (0 = greedy)");
@@ -933,7 +935,7 @@ struct Engine {
 
     int decode(int n, int use_graph) {
         LLMI_REQUIRE(prompt_len > 0, "decode: set_prompt first");
-        LLMI_REQUIRE(c.tp_world == 1 || comm || xchg_mode >= 1,
+        LLMI_REQUIRE(c.tp_world == 1 || comm || xchg_mode >= 1 || xchg_loop,
                      "decode: tp_world > 1 needs an RCCL id at create or the one-shot exchange (xchg_open + set_exchange)");
         LLMI_REQUIRE(n >= 0 && host_next_pos + n <= c.max_seq, "decode: would run past max_seq");
         if (decode_mode == 1 && n > 0) LLMI_TRY(prepare_ring());
@@ -1594,6 +1596,19 @@ int llmi_engine_xchg_open(llmi_engine* e, const void* handles) {
     }
     LLMI_TRY(g.set_peers(p));
     g.peers_ready = true;
+    return LLMI_OK;
+}
+
+int llmi_engine_xchg_loopback(llmi_engine* e) {
+    LLMI_REQUIRE(e, "xchg_loopback: null engine");
+    Engine& g = e->e;
+    LLMI_REQUIRE(!g.grouped && !g.comm, "xchg_loopback: not on a group rank or an engine with an RCCL communicator");
+    LLMI_REQUIRE(!g.peers_ready, "xchg_loopback: the peer exchange is already open");
+    LLMI_HIP(hipSetDevice(g.device));
+    LLMI_TRY(g.alloc_xchg());
+    LLMI_TRY(g.set_peers(std::vector<char*>(g.c.tp_world, g.inbox)));
+    g.peers_ready = true;
+    g.xchg_loop = 1;
     return LLMI_OK;
 }
 

@@ -29,6 +29,11 @@ struct XchgArgs {
     int* err = nullptr;               // DecodeState::error; bit 8 = a peer never arrived (timeout)
     int mode = 3;                     // 1: push only, 2: wait + reduce only, 3: both
     int cap_n = 0, cap_w = 0;         // inbox geometry: elements per slot, slots per phase
+    // loopback (one-GPU pricing of a rank's exchange, llmi_engine_xchg_loopback): every peer is
+    // this rank's own inbox; the push fills slot / flag [ph][q] for every q (this rank's vector
+    // in its own slot, zeros in the others: the same W x n x 8 bytes of writes as a real push),
+    // so the reduce finds all W arrivals and sums to this rank's own partial
+    int loop = 0;
 };
 
 struct GemvArgs {

@@ -41,13 +41,18 @@ __device__ __forceinline__ void push_slice(const XchgArgs& a, int g, unsigned lo
         } else {
             v.x = a.buf[i0];
         }
-        for (int q = 0; q < a.world; ++q) *reinterpret_cast<longlong2*>(slot_of(a, a.peers[q], ph, a.rank) + i0) = v;
+        for (int q = 0; q < a.world; ++q) {
+            const bool zero = a.loop && q != a.rank;  // loopback: the other ranks' slots get zeros
+            *reinterpret_cast<longlong2*>(slot_of(a, a.peers[q], ph, a.loop ? q : a.rank) + i0) =
+                zero ? make_longlong2(0, 0) : v;
+        }
     }
     __threadfence_system();  // every lane's data is visible system-wide ...
     __syncthreads();         // ... before one lane raises the flags
     if (threadIdx.x == 0)
         for (int q = 0; q < a.world; ++q)
-            __hip_atomic_store(flag_of(a, a.peers[q], ph, a.rank, g), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(flag_of(a, a.peers[q], ph, a.loop ? q : a.rank, g), e, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Wait until every rank's slice g of exchange e arrived in this rank's inbox, sum (op 0) /

@@ -108,6 +108,7 @@ _SIGS = {
     "llmi_engine_debug_set_next_pos": (_I, [_P, _I]),
     "llmi_engine_xchg_handle": (_I, [_P, _P]),
     "llmi_engine_xchg_open": (_I, [_P, _P]),
+    "llmi_engine_xchg_loopback": (_I, [_P]),
     "llmi_engine_set_exchange": (_I, [_P, _I]),
     "llmi_engine_set_decode_mode": (_I, [_P, _I]),
     "llmi_group_set_exchange": (_I, [_P, _I]),

@@ -150,6 +150,12 @@ class Engine:
         buf = C.create_string_buffer(blob, len(blob))
         call("llmi_engine_xchg_open", self._h, buf)
 
+    def xchg_loopback(self):
+        """Price ONE tensor-parallel rank on one GPU (llmi_engine_xchg_loopback): every peer
+        inbox is this rank's own; the timing and launch structure are a rank's, the tokens
+        are not the TP model's. Then set_exchange(0 | 1 | 2)."""
+        call("llmi_engine_xchg_loopback", self._h)
+
     def set_exchange(self, mode: int):
         """0: RCCL all-reduces (needs a tp_id at create); 1: the one-shot peer exchange;
         2: the same exchange fused into the producing launches (o_proj / down / lm_head)."""

@@ -95,3 +95,29 @@ def test_oneshot_two_processes_one_gpu_ipc(tmp_path, mode):
     cfg.kv_dtype = _lib.F32
     _, _, _, lg, _ = group_run("tiny.npz", cfg, 2, 0, True)
     np.testing.assert_array_equal(np.concatenate([r["logits"] for r in res]), lg)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_rank_exchange_modes_agree_bitwise(world):
+    """llmi_engine_xchg_loopback (the one-GPU pricing of a single TP rank): every peer inbox is
+    the rank's own, the push writes its partial into its own slot and zeros into the others,
+    so the one-shot exchange (mode 1) and the producer-fused tail (mode 2) must reduce to the
+    rank's own partial -- tokens, logits and hidden state bitwise those of running with no
+    exchange at all (mode 0), graph replay and eager alike."""
+    from llmi.engine import Engine
+    cfg = preset("llama2-7b", layers=2, max_seq=160, tp_rank=0, tp_world=world)
+    out = {}
+    with Engine(cfg) as e:
+        e.load_synthetic(3)
+        e.xchg_loopback()
+        prompt = np.array([1, 5, 9, 13, 17, 21, 25, 29], np.int32)
+        for mode in (0, 1, 2):
+            e.set_exchange(mode)
+            for graph in (True, False):
+                toks = e.generate(prompt, 70, use_graph=graph)  # crosses a split-count boundary
+                out[(mode, graph)] = (toks.copy(), e.logits().copy(), e.hidden().copy())
+    ref = out[(0, True)]
+    for k, v in out.items():
+        np.testing.assert_array_equal(v[0], ref[0], err_msg=str(k))
+        np.testing.assert_array_equal(v[1], ref[1], err_msg=str(k))
+        np.testing.assert_array_equal(v[2], ref[2], err_msg=str(k))
