@@ -734,6 +734,7 @@ struct Engine {
     int alloc_xchg() {
         if (inbox) return LLMI_OK;
         const int W = c.tp_world;
+        LLMI_REQUIRE(W <= kXchgMaxWorld, "xchg: the one-shot exchange takes at most 8 ranks");
         xchg_cap_n = std::max(c.hidden, lm_grid);
         xchg_cap_n += xchg_cap_n & 1;
         LLMI_REQUIRE(xchg_cap_n <= kXchgSlice * kXchgMaxSlices, "xchg: hidden / lm_head partials exceed the inbox");

@@ -427,6 +427,7 @@ int repeat_kv_launch(const void* k_cache, const void* v_cache, int dtype, int la
 // --------------------------------------------- one-shot TP exchange (xchg.hip)
 constexpr int kXchgSlice = 256;     // vector elements per workgroup
 constexpr int kXchgMaxSlices = 64;  // n <= 16384 elements
+constexpr int kXchgMaxWorld = 8;    // ranks of one exchange (one node's GPUs)
 size_t xchg_inbox_bytes(int world, int cap_n);
 int xchg_launch(const XchgArgs& a, hipStream_t s);
 

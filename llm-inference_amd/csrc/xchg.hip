@@ -47,7 +47,8 @@ size_t xchg_inbox_bytes(int world, int cap_n) {
 
 int xchg_launch(const XchgArgs& a, hipStream_t s) {
     LLMI_REQUIRE(a.buf && a.peers && a.ep && a.err, "xchg: null pointer");
-    LLMI_REQUIRE(a.world >= 1 && a.world <= a.cap_w && a.rank >= 0 && a.rank < a.world, "xchg: bad rank/world");
+    LLMI_REQUIRE(a.world >= 1 && a.world <= a.cap_w && a.world <= kXchgMaxWorld && a.rank >= 0 && a.rank < a.world,
+                 "xchg: bad rank/world (at most 8 ranks)");
     LLMI_REQUIRE(a.n >= 0 && a.n <= a.cap_n && a.n <= kXchgSlice * kXchgMaxSlices, "xchg: n exceeds the inbox");
     LLMI_REQUIRE(a.cap_n % 2 == 0, "xchg: inbox slots must hold an even element count (16-B accesses)");
     LLMI_REQUIRE(a.op == 0 || a.op == 2, "xchg: op must be 0 (int64 sum) or 2 (uint64 max)");

@@ -23,14 +23,33 @@ __device__ __forceinline__ long long ld_agent(const long long* p) {
                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Write-through (system-coherent, sc0 sc1) 8-B store / load: the inboxes are uncached HBM,
+// local or a peer's over xGMI, so these reach memory without any L2 write-back or invalidate
+// (a system-scope release / acquire fence costs a whole-L2 wbl2 / inv per wave: with one per
+// flag store and per wave, an exchange cost ~10 us on one GPU, r05a)
+__device__ __forceinline__ void st_sys(long long* p, long long v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ long long ld_sys(const long long* p) {
+    return (long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<long long*>(p)),
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Push slice g (elements [g * kXchgSlice, ...) of a.buf) into slot [ph][rank] of every
 // inbox, then raise flag [ph][rank][g] = e in every inbox. Block-wide (every thread calls).
 // AGENT: read buf with agent-scope loads (its values were produced inside this launch by
 // other workgroups' device-scope atomics / released stores).
+// Ordering without fences: every payload store is write-through; each wave waits for its
+// stores' acknowledgements (vmcnt 0: the data is in the target's memory), the barrier orders
+// that before thread 0's flag stores, which are write-through too.
 template <bool AGENT>
 __device__ __forceinline__ void push_slice(const XchgArgs& a, int g, unsigned long long e) {
     const int ph = (int)(e & 1ull);
     const int i_end = min(a.n, (g + 1) * kXchgSlice);
+    char* peer[kXchgMaxWorld];  // every inbox base, loaded together (one round trip, not one per rank)
+#pragma unroll
+    for (int q = 0; q < kXchgMaxWorld; ++q) peer[q] = a.peers[q < a.world ? q : 0];
     for (int i0 = g * kXchgSlice + 2 * (int)threadIdx.x; i0 < i_end; i0 += 2 * (int)blockDim.x) {
         longlong2 v = make_longlong2(0, 0);
         if constexpr (AGENT) {
@@ -41,23 +60,31 @@ __device__ __forceinline__ void push_slice(const XchgArgs& a, int g, unsigned lo
         } else {
             v.x = a.buf[i0];
         }
-        for (int q = 0; q < a.world; ++q) {
+#pragma unroll
+        for (int q = 0; q < kXchgMaxWorld; ++q) {
+            if (q >= a.world) break;
             const bool zero = a.loop && q != a.rank;  // loopback: the other ranks' slots get zeros
-            *reinterpret_cast<longlong2*>(slot_of(a, a.peers[q], ph, a.loop ? q : a.rank) + i0) =
-                zero ? make_longlong2(0, 0) : v;
+            long long* d = slot_of(a, peer[q], ph, a.loop ? q : a.rank) + i0;
+            st_sys(d, zero ? 0ll : v.x);
+            st_sys(d + 1, zero ? 0ll : v.y);
         }
     }
-    __threadfence_system();  // every lane's data is visible system-wide ...
-    __syncthreads();         // ... before one lane raises the flags
-    if (threadIdx.x == 0)
-        for (int q = 0; q < a.world; ++q)
-            __hip_atomic_store(flag_of(a, a.peers[q], ph, a.loop ? q : a.rank, g), e, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload acknowledged
+    __syncthreads();                                    // ... every wave's, before the flags
+    if ((int)threadIdx.x < a.world) {  // one lane per rank raises that inbox's flag
+        char* pb = peer[0];
+#pragma unroll
+        for (int q = 1; q < kXchgMaxWorld; ++q)
+            if ((int)threadIdx.x == q) pb = peer[q];
+        __hip_atomic_store(flag_of(a, pb, ph, a.loop ? (int)threadIdx.x : a.rank, g), e, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Wait until every rank's slice g of exchange e arrived in this rank's inbox, sum (op 0) /
 // max (op 2) the W slots in rank order into a.buf, and record e as slice g's epoch.
 // Block-wide. A peer that never arrives: error bit 8 (tokens_out raises), later waits skip.
+// The W slot loads are all issued before the first is used (one memory round trip, not W).
 __device__ __forceinline__ void reduce_slice(const XchgArgs& a, int g, unsigned long long e) {
     const int ph = (int)(e & 1ull);
     char* own = a.peers[a.rank];
@@ -76,18 +103,26 @@ __device__ __forceinline__ void reduce_slice(const XchgArgs& a, int g, unsigned 
             }
         }
     }
-    __syncthreads();
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the slots written by the peers
+    __syncthreads();  // the flags were seen before any slot is read (write-through loads below)
     const int i_end = min(a.n, (g + 1) * kXchgSlice);
     for (int i0 = g * kXchgSlice + 2 * (int)threadIdx.x; i0 < i_end; i0 += 2 * (int)blockDim.x) {
+        long long v0[kXchgMaxWorld], v1[kXchgMaxWorld];
+#pragma unroll
+        for (int q = 0; q < kXchgMaxWorld; ++q) {
+            const long long* sp = slot_of(a, own, ph, q < a.world ? q : 0) + i0;
+            v0[q] = ld_sys(sp);
+            v1[q] = ld_sys(sp + 1);
+        }
         long long s0 = 0, s1 = 0;
         unsigned long long m0 = 0, m1 = 0;
-        for (int q = 0; q < a.world; ++q) {
-            const longlong2 v = *reinterpret_cast<const longlong2*>(slot_of(a, own, ph, q) + i0);
-            s0 += v.x;
-            s1 += v.y;
-            m0 = max(m0, (unsigned long long)v.x);
-            m1 = max(m1, (unsigned long long)v.y);
+#pragma unroll
+        for (int q = 0; q < kXchgMaxWorld; ++q) {
+            if (q < a.world) {
+                s0 += v0[q];
+                s1 += v1[q];
+                m0 = max(m0, (unsigned long long)v0[q]);
+                m1 = max(m1, (unsigned long long)v1[q]);
+            }
         }
         a.buf[i0] = a.op == 0 ? s0 : (long long)m0;
         if (i0 + 1 < a.n) a.buf[i0 + 1] = a.op == 0 ? s1 : (long long)m1;

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--decode-mode", type=int, default=0)
+    ap.add_argument("--eager", action="store_true", help="launch eagerly (rocprofv3 kernel traces of graph "
+                                                          "replays crash on ROCm 7.2)")
     args = ap.parse_args()
     for W in [int(w) for w in args.worlds.split(",")]:
         cfg = preset("llama2-7b", max_seq=args.max_seq, layers=args.layers, tp_rank=0, tp_world=W)
@@ -55,13 +57,13 @@ def main():
                     e.set_prompt(prompt)
                     e.sync()
                     t0 = time.perf_counter()
-                    e.decode(args.max_seq, use_graph=True)
+                    e.decode(args.max_seq, use_graph=not args.eager)
                     e.sync()
                     dt = time.perf_counter() - t0
                     if rep > 0:
                         best = dt if best is None else min(best, dt)
                 us_tok = best / args.max_seq * 1e6
-                print(json.dumps({"tp_world": W, "exchange_mode": mode, "decode_mode": args.decode_mode,
+                print(json.dumps({"tp_world": W, "exchange_mode": mode, "decode_mode": args.decode_mode, "graph": not args.eager,
                                   "layers": args.layers, "max_seq": args.max_seq,
                                   "us_per_token_per_rank": round(us_tok, 2),
                                   "us_per_layer": round(us_tok / args.layers, 2),
