@@ -25,12 +25,42 @@ from llmi import _lib  # noqa: E402
 from llmi.engine import Engine, preset, synth_prompt  # noqa: E402
 from llmi.timeline import analyse, slot_wgs  # noqa: E402
 
+def wg_detail(host, stride, layer):
+    """Per-workgroup start / end (us from the launch's first start), the XCD (blockIdx % 8,
+    round-robin dispatch) and the hardware CU id, for layer `layer`'s q/k/v, o and down, plus
+    per-XCD completion quantiles: where a launch's tail comes from."""
+    out = {}
+    for k, off in (("qkv", 0), ("o", 2), ("down", 4)):
+        s = 5 * layer + off
+        rows = host[s * stride:(s + 1) * stride].astype(np.int64)
+        idx = np.nonzero(rows[:, 0] > 0)[0]
+        v = rows[idx]
+        t0 = v[:, 0].min()
+        start, end = (v[:, 0] - t0) / 100.0, (v[:, 3] - t0) / 100.0
+        xcd = idx % 8
+        per_xcd = {}
+        for x in range(8):
+            e = end[xcd == x]
+            if len(e):
+                per_xcd[str(x)] = [round(float(q), 2) for q in np.quantile(e, [0, 0.5, 0.9, 1.0])]
+        out[k] = {"n": int(len(idx)), "end_quantiles_us": [round(float(q), 2) for q in
+                                                            np.quantile(end, [0, 0.1, 0.5, 0.9, 0.99, 1.0])],
+                  "start_max_us": round(float(start.max()), 2),
+                  "end_quantiles_by_xcd_us [min, p50, p90, max]": per_xcd,
+                  "wg": [[int(i), round(float(a), 2), round(float(b), 2), int(r[4])]
+                         for i, a, b, r in zip(idx, start, end, v)]}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ctx", default="8,512,1024,2047")
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--out", default="")
+    ap.add_argument("--wg-layer", type=int, default=-1,
+                    help="also dump layer L's per-workgroup {start, end, xcd, cu} for q/k/v, o and down, "
+                         "with completion quantiles per XCD (VERDICT r04 item 3a)")
     a = ap.parse_args()
     lib = _lib.lib()
     cfg = preset(a.preset, layers=a.layers, max_seq=2048)
@@ -58,6 +88,8 @@ def main():
             e.sync()
             lib.llmi_memcpy(host.ctypes.data_as(C.c_void_p), buf, C.c_size_t(nbytes), 1)
             r = analyse(host, n_slots, stride, a.layers)
+            if a.wg_layer >= 0:
+                r["workgroups"] = wg_detail(host, stride, a.wg_layer)
             res["ctx"][str(c)] = r
             print(c, json.dumps(r), flush=True)
         lib.llmi_engine_debug_timeline(e._h, None, C.c_size_t(0), 0)
