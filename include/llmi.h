@@ -489,6 +489,12 @@ int llmi_engine_xchg_open(llmi_engine* e, const void* handles);
  * exchange at all (the compute-only floor), 1 the one-shot exchange launches, 2 the
  * exchange fused into the producers. */
 int llmi_engine_xchg_loopback(llmi_engine* e);
+
+/* Engine tuning switches for same-process A/B (no reference counterpart); the captured
+ * token graphs are rebuilt on the next decode. "steal": GEMV tail work stealing -- 0 off,
+ * 1 q/k/v + gate_up (row groups past the first wave round handed out from XCD-mixed ticket
+ * shards), 2 down (its last batch of every row pair), 3 both. */
+int llmi_engine_set_option(llmi_engine* e, const char* name, int value);
 int llmi_engine_set_exchange(llmi_engine* e, int mode);
 /* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built
  * afterwards) write a per-workgroup timeline into dev_buf (8 x uint64 per

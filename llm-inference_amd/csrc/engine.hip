@@ -209,10 +209,16 @@ struct Engine {
     // stochastic sampling (Llama<T>::Sampling, llama.cpp:245-262): 0 = greedy argmax
     int sample_k = 0;
     uint64_t sample_seed = 0;
+    // GEMV tail work stealing (gemv_impl.h, GemvArgs::steal): 0 off, bit 0 q/k/v + gate_up
+    // (row groups past the first wave round), bit 1 down (its last batch per row pair);
+    // one counter block, left zero by every launch (launches on the stream never overlap)
+    int steal_mode = 0;
+    unsigned* steal_blk = nullptr;
     int32_t* samp_ids = nullptr;
     float* samp_vals = nullptr;
 
     ~Engine() {  // teardown errors are not actionable; ignore them explicitly
+        if (steal_blk) (void)hipFree(steal_blk);
         if (samp_ids) (void)hipFree(samp_ids);
         if (samp_vals) (void)hipFree(samp_vals);
         graphs.clear();
@@ -622,6 +628,7 @@ struct Engine {
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
+        if (steal_mode & 1) a.steal = steal_blk;
         return a;
     }
     AttnArgs attn_args(int l) const {
@@ -671,6 +678,7 @@ struct Engine {
         a.seed_keep = c.tp_rank == 0 ? 1 : 0;
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
+        if (steal_mode & 1) a.steal = steal_blk;
         return a;
     }
     GemvArgs down_args(int l) const {
@@ -685,6 +693,10 @@ struct Engine {
         a.ksplit = (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT
                    : (wdt == LLMI_F16 && il % (8 * LLMI_F16_DOWN_KSPLIT) == 0) ? LLMI_F16_DOWN_KSPLIT
                                                                                : 1;
+        if ((steal_mode & 2) && a.ksplit == 1) {
+            a.steal = steal_blk;
+            a.steal_tail = 1;
+        }
         return a;
     }
 
@@ -788,6 +800,21 @@ struct Engine {
         graphs.clear();  // the captured steps change
         xchg_mode = mode;
         tail_mode = mode == 2 ? 3 : 0;
+        return LLMI_OK;
+    }
+    int set_option(const std::string& name, int value) {
+        LLMI_HIP(hipStreamSynchronize(stream));
+        if (name == "steal") {
+            LLMI_REQUIRE(value >= 0 && value <= 3, "set_option steal: 0 off, 1 q/k/v + gate_up, 2 down, 3 both");
+            if (value && !steal_blk) {
+                LLMI_HIP(hipMalloc(&steal_blk, kStealWords * sizeof(unsigned)));
+                LLMI_HIP(hipMemset(steal_blk, 0, kStealWords * sizeof(unsigned)));
+            }
+            steal_mode = value;
+        } else {
+            LLMI_REQUIRE(false, "set_option: unknown option (steal)");
+        }
+        graphs.clear();  // the captured steps change
         return LLMI_OK;
     }
     bool peers_ready = false;
@@ -1598,6 +1625,12 @@ int llmi_engine_xchg_open(llmi_engine* e, const void* handles) {
     LLMI_TRY(g.set_peers(p));
     g.peers_ready = true;
     return LLMI_OK;
+}
+
+int llmi_engine_set_option(llmi_engine* e, const char* name, int value) {
+    LLMI_REQUIRE(e && name, "set_option: null argument");
+    LLMI_HIP(hipSetDevice(e->e.device));
+    return e->e.set_option(name, value);
 }
 
 int llmi_engine_xchg_loopback(llmi_engine* e) {

@@ -64,6 +64,8 @@ int gemv_launch(const GemvArgs& a, hipStream_t s) {
                                          a.k % (a.ksplit * epl) == 0),
                  "gemv: EPI_ATOMIC needs yacc, an fp32 x and k divisible into ksplit 16-B slices");
     LLMI_REQUIRE(a.epi == EPI_ATOMIC || a.ksplit == 1, "gemv: ksplit only with EPI_ATOMIC");
+    LLMI_REQUIRE(!a.steal || (a.ksplit == 1 && a.steal_tail >= 0 && (a.steal_tail == 0 || a.epi == EPI_ATOMIC)),
+                 "gemv: work stealing needs ksplit 1 (a batch tail only with the atomic epilogue)");
     LLMI_REQUIRE(a.ldw == 0 || a.ldw >= a.k, "gemv: ldw < k");
     const int grid = gemv_grid(a);
     switch (a.w_dtype) {

@@ -310,21 +310,77 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
             }
         }
     }
+    constexpr int B = kWave * kUnroll;  // chunks per batch
+    // tail work stealing (GemvArgs::steal): the static part is each wave's first group only
+    // (EPI_ATOMIC: without its last steal_tail batches); see the dynamic part below
+    const bool steal = !PIPE && a.steal != nullptr;
+    const int nbatch = (nc + B - 1) / B;
+    const int tailb = (steal && EPI == EPI_ATOMIC) ? min(a.steal_tail, nbatch - 1) : 0;
+    const int nc_static = (nbatch - tailb) * B;
     // ---- first group (its first batch is already in flight)
     if (!PIPE && g0 < n_groups) {
         float acc[ROWS];
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
         dot_batch(w0, 0, acc);
-        for (int base = kWave * kUnroll; base < nc; base += kWave * kUnroll) {
+        for (int base = B; base < nc_static; base += B) {
             uint4 wv[ROWS][kUnroll];
             load_batch(wv, rows0, base);
             dot_batch(wv, base, acc);
         }
         finish(g0, rows0, acc);
     }
-    // ---- remaining groups
-    for (int g = g0 + nblk * kWavesPerBlock; !PIPE && g < n_groups; g += nblk * kWavesPerBlock) {
+    if (steal && (tailb ? min(n_groups, nblk * kWavesPerBlock) : n_groups - nblk * kWavesPerBlock) > 0) {
+        // Dynamic units of one workgroup (a group per wave): EPI_ATOMIC with a tail, unit u =
+        // the last tailb batches of groups 4u .. 4u + 3 (the partial sums are exact int64 adds,
+        // so who adds them does not matter); otherwise unit u = groups W + 4u .. W + 4u + 3.
+        // Tickets: shard (bid / 8) % S is shared by 8 consecutive workgroups, one per XCD;
+        // it owns units s, s + S, ... One ticket per unit plus one past the end per workgroup,
+        // prefetched a unit ahead; the shard's last workgroup to leave re-zeroes it.
+        const int W = nblk * kWavesPerBlock;
+        const int ngs = tailb ? min(n_groups, W) : max(n_groups - W, 0);
+        const int U = (ngs + kWavesPerBlock - 1) / kWavesPerBlock;
+        const int NS = min(kStealShards, max(1, nblk / 8));
+        const int sh = (bid >> 3) % NS;
+        unsigned* tick = a.steal + sh * 32;
+        unsigned* left = a.steal + (kStealShards + sh) * 32;
+        __shared__ unsigned tick_s;
+        auto take = [&]() { return __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        unsigned t = 0;
+        if (tid == 0) t = take();
+        for (;;) {
+            if (tid == 0) tick_s = t;
+            __syncthreads();
+            const int u = sh + NS * (int)tick_s;
+            __syncthreads();  // tick_s read by every wave before thread 0 may overwrite it
+            if (u >= U) break;
+            if (tid == 0) t = take();  // the next unit's ticket, in flight during this one
+            const int g = (tailb ? 0 : W) + u * kWavesPerBlock + wave;
+            if (g < n_groups && (!tailb || g < W)) {
+                int rows[ROWS];
+                rows_of(g, rows);
+                float acc[ROWS];
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+                for (int base = tailb ? nc_static : 0; base < nc; base += B) {
+                    uint4 wv[ROWS][kUnroll];
+                    load_batch(wv, rows, base);
+                    dot_batch(wv, base, acc);
+                }
+                finish(g, rows, acc);
+            }
+        }
+        if (tid == 0) {
+            int members = 0;  // workgroups of this shard: groups of 8 k = sh, sh + NS, ...
+            for (int k = sh; k * 8 < nblk; k += NS) members += min(8, nblk - k * 8);
+            if (__hip_atomic_fetch_add(left, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1) {
+                __hip_atomic_store(tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(left, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    // ---- remaining groups (no stealing: every wave's later groups, statically)
+    for (int g = g0 + nblk * kWavesPerBlock; !PIPE && !steal && g < n_groups; g += nblk * kWavesPerBlock) {
         int rows[ROWS];
         rows_of(g, rows);
         float acc[ROWS];

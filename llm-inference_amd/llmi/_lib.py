@@ -109,6 +109,7 @@ _SIGS = {
     "llmi_engine_xchg_handle": (_I, [_P, _P]),
     "llmi_engine_xchg_open": (_I, [_P, _P]),
     "llmi_engine_xchg_loopback": (_I, [_P]),
+    "llmi_engine_set_option": (_I, [_P, C.c_char_p, _I]),
     "llmi_engine_set_exchange": (_I, [_P, _I]),
     "llmi_engine_set_decode_mode": (_I, [_P, _I]),
     "llmi_group_set_exchange": (_I, [_P, _I]),

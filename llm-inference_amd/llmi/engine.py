@@ -150,6 +150,10 @@ class Engine:
         buf = C.create_string_buffer(blob, len(blob))
         call("llmi_engine_xchg_open", self._h, buf)
 
+    def set_option(self, name: str, value: int):
+        """llmi_engine_set_option: tuning switches for same-process A/B ("steal": 0..3)."""
+        call("llmi_engine_set_option", self._h, name.encode(), int(value))
+
     def xchg_loopback(self):
         """Price ONE tensor-parallel rank on one GPU (llmi_engine_xchg_loopback): every peer
         inbox is this rank's own; the timing and launch structure are a rank's, the tokens

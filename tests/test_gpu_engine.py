@@ -203,3 +203,35 @@ def test_host_device_position_mismatch_is_reported(use_graph):
         e.decode(1, use_graph=use_graph)
         with pytest.raises(_lib.LlmiError, match="device error flag 4"):
             e.tokens()
+
+
+@pytest.mark.parametrize("steal", [1, 2, 3])
+def test_gemv_work_stealing_matches_fixture_and_is_repeatable(steal):
+    """GEMV tail work stealing (llmi_engine_set_option "steal"): q/k/v and gate_up hand their
+    row groups past the first wave round to whichever workgroup asks first (each group still
+    computed whole by one wave: bitwise the static result), down hands out the last batch of
+    every row pair (its partial sums added as exact int64: deterministic, a different fp32
+    association from the static kernel). F3: tokens exact, logits within 1e-3 of the reference;
+    graph replay equals eager launches bitwise, across split-count boundaries; mode 1 is
+    bitwise the static kernels."""
+    f = load("f3_decode.npz")
+    cfg = preset("llama2-7b", layers=2, max_seq=160)
+    cfg.kv_dtype = _lib.F32
+    out = {}
+    with Engine(cfg) as e:
+        e.load_synthetic(int(f["seed"]))
+        for st in (0, steal):
+            e.set_option("steal", st)
+            for g in (True, False):
+                toks = e.generate(f["prompt"], 140, use_graph=g)
+                out[(st, g)] = (toks.copy(), e.logits().copy())
+    np.testing.assert_array_equal(out[(steal, True)][0][:len(f["tokens"])], f["tokens"])
+    np.testing.assert_array_equal(out[(steal, True)][0], out[(0, True)][0])
+    np.testing.assert_array_equal(out[(steal, True)][1], out[(steal, False)][1])
+    np.testing.assert_array_equal(out[(steal, True)][0], out[(steal, False)][0])
+    r = rel(out[(steal, True)][1], out[(0, True)][1])
+    print(f"steal {steal}: logits rel-L2 vs static {r:.2e}")
+    if steal == 1:
+        assert r == 0.0
+    else:
+        assert r < 1e-5
