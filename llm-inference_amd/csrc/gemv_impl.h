@@ -148,6 +148,13 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
         }
     };
 
+    // tail work stealing: this workgroup's first ticket, requested before anything else so
+    // its round trip overlaps the static part (see the dynamic part below)
+    const int NS = min(kStealShards, max(1, nblk / 8));
+    const int sh = (bid >> 3) % NS;
+    unsigned first_ticket = 0;
+    if (a.steal != nullptr && tid == 0)
+        first_ticket = __hip_atomic_fetch_add(a.steal + sh * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- prologue. Issue order matters: vmcnt retires loads in issue order, so x
     // (and gamma) go first, then this wave's first weight batch; the weight stream is
     // then in flight while x is staged and the norm is reduced.
@@ -330,7 +337,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
         }
         finish(g0, rows0, acc);
     }
-    if (steal && (tailb ? min(n_groups, nblk * kWavesPerBlock) : n_groups - nblk * kWavesPerBlock) > 0) {
+    if (steal) {
         // Dynamic units of one workgroup (a group per wave): EPI_ATOMIC with a tail, unit u =
         // the last tailb batches of groups 4u .. 4u + 3 (the partial sums are exact int64 adds,
         // so who adds them does not matter); otherwise unit u = groups W + 4u .. W + 4u + 3.
@@ -340,14 +347,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
         const int W = nblk * kWavesPerBlock;
         const int ngs = tailb ? min(n_groups, W) : max(n_groups - W, 0);
         const int U = (ngs + kWavesPerBlock - 1) / kWavesPerBlock;
-        const int NS = min(kStealShards, max(1, nblk / 8));
-        const int sh = (bid >> 3) % NS;
         unsigned* tick = a.steal + sh * 32;
         unsigned* left = a.steal + (kStealShards + sh) * 32;
         __shared__ unsigned tick_s;
         auto take = [&]() { return __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-        unsigned t = 0;
-        if (tid == 0) t = take();
+        unsigned t = first_ticket;  // taken at the kernel start
         for (;;) {
             if (tid == 0) tick_s = t;
             __syncthreads();
