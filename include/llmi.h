@@ -491,9 +491,9 @@ int llmi_engine_xchg_open(llmi_engine* e, const void* handles);
 int llmi_engine_xchg_loopback(llmi_engine* e);
 
 /* Engine tuning switches for same-process A/B (no reference counterpart); the captured
- * token graphs are rebuilt on the next decode. "steal": GEMV tail work stealing -- 0 off,
- * 1 q/k/v + gate_up (row groups past the first wave round handed out from XCD-mixed ticket
- * shards), 2 down (its last batch of every row pair), 3 both. */
+ * token graphs are rebuilt on the next decode. "kpar": 1 (default) lets a TP rank's q/k/v and
+ * gate_up GEMVs split K over 2 or 4 waves of a workgroup when one row group per wave would
+ * leave CUs idle or doubled (tp_world > 1 only), 0 keeps one wave per row group. */
 int llmi_engine_set_option(llmi_engine* e, const char* name, int value);
 int llmi_engine_set_exchange(llmi_engine* e, int mode);
 /* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built

@@ -209,16 +209,10 @@ struct Engine {
     // stochastic sampling (Llama<T>::Sampling, llama.cpp:245-262): 0 = greedy argmax
     int sample_k = 0;
     uint64_t sample_seed = 0;
-    // GEMV tail work stealing (gemv_impl.h, GemvArgs::steal): 0 off, bit 0 q/k/v + gate_up
-    // (row groups past the first wave round), bit 1 down (its last batch per row pair);
-    // one counter block, left zero by every launch (launches on the stream never overlap)
-    int steal_mode = 0;
-    unsigned* steal_blk = nullptr;
     int32_t* samp_ids = nullptr;
     float* samp_vals = nullptr;
 
     ~Engine() {  // teardown errors are not actionable; ignore them explicitly
-        if (steal_blk) (void)hipFree(steal_blk);
         if (samp_ids) (void)hipFree(samp_ids);
         if (samp_vals) (void)hipFree(samp_vals);
         graphs.clear();
@@ -272,6 +266,7 @@ struct Engine {
                      "engine: hidden, q rows per rank and inter per rank must be multiples of 16 bytes");
 
         LLMI_HIP(hipSetDevice(device));
+        LLMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
         if (ext_stream) {
             stream = ext_stream;
             own_stream = false;
@@ -620,6 +615,18 @@ struct Engine {
         return a;
     }
 
+    // K split inside the workgroup for row-group counts that leave CUs idle or doubled with
+    // one group per wave (a TP rank's q/k/v and gate_up): 4 waves per group below one
+    // workgroup per CU, 2 below two; TP 1 shapes never qualify (tp_world 1 keeps kpar off so
+    // its sums stay bitwise those of the fixtures' runs)
+    int kpar_of(int groups) const {
+        if (c.tp_world == 1 || kpar_off) return 0;
+        const int cus = n_cu > 0 ? n_cu : 256;
+        const int blocks = (groups + 3) / 4;
+        return blocks < cus ? 4 : blocks < 2 * cus ? 2 : 0;
+    }
+    bool kpar_off = false;
+
     GemvArgs qkv_args(int l) const {
         const Layer& L = layers[l];
         GemvArgs a;
@@ -628,7 +635,7 @@ struct Engine {
         a.n_rows = ql + 2 * kvrows; a.k = c.hidden;
         a.x_fixed = res[l % 2]; a.gamma = L.attn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_STORE; a.y = qkv_buf;
-        if (steal_mode & 1) a.steal = steal_blk;
+        a.kpar = kpar_of((a.n_rows + 1) / 2);
         return a;
     }
     AttnArgs attn_args(int l) const {
@@ -678,7 +685,7 @@ struct Engine {
         a.seed_keep = c.tp_rank == 0 ? 1 : 0;
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
-        if (steal_mode & 1) a.steal = steal_blk;
+        a.kpar = kpar_of(il);
         return a;
     }
     GemvArgs down_args(int l) const {
@@ -693,10 +700,6 @@ struct Engine {
         a.ksplit = (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT
                    : (wdt == LLMI_F16 && il % (8 * LLMI_F16_DOWN_KSPLIT) == 0) ? LLMI_F16_DOWN_KSPLIT
                                                                                : 1;
-        if ((steal_mode & 2) && a.ksplit == 1) {
-            a.steal = steal_blk;
-            a.steal_tail = 1;
-        }
         return a;
     }
 
@@ -804,15 +807,11 @@ struct Engine {
     }
     int set_option(const std::string& name, int value) {
         LLMI_HIP(hipStreamSynchronize(stream));
-        if (name == "steal") {
-            LLMI_REQUIRE(value >= 0 && value <= 3, "set_option steal: 0 off, 1 q/k/v + gate_up, 2 down, 3 both");
-            if (value && !steal_blk) {
-                LLMI_HIP(hipMalloc(&steal_blk, kStealWords * sizeof(unsigned)));
-                LLMI_HIP(hipMemset(steal_blk, 0, kStealWords * sizeof(unsigned)));
-            }
-            steal_mode = value;
+        if (name == "kpar") {
+            LLMI_REQUIRE(value == 0 || value == 1, "set_option kpar: 1 on (default), 0 off");
+            kpar_off = value == 0;
         } else {
-            LLMI_REQUIRE(false, "set_option: unknown option (steal)");
+            LLMI_REQUIRE(false, "set_option: unknown option (kpar)");
         }
         graphs.clear();  // the captured steps change
         return LLMI_OK;

@@ -41,6 +41,7 @@ int epl_of(int dt) { return dt == LLMI_F16 ? 8 : dt == LLMI_F32 ? 4 : dt == LLMI
 int gemv_grid(const GemvArgs& a) {
     if (a.grid > 0) return a.grid;
     const int groups = (a.epi == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + kRows - 1) / kRows;
+    if (a.kpar > 1) return (groups + kWavesPerBlock / a.kpar - 1) / (kWavesPerBlock / a.kpar);  // a group per wave
     int blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     // cap (default ~4 workgroups per CU on 256 CUs); waves then loop over several row groups
     const int S = (a.epi == EPI_ATOMIC) ? a.ksplit : 1;  // split-K: S workgroups per row-group block
@@ -64,8 +65,9 @@ int gemv_launch(const GemvArgs& a, hipStream_t s) {
                                          a.k % (a.ksplit * epl) == 0),
                  "gemv: EPI_ATOMIC needs yacc, an fp32 x and k divisible into ksplit 16-B slices");
     LLMI_REQUIRE(a.epi == EPI_ATOMIC || a.ksplit == 1, "gemv: ksplit only with EPI_ATOMIC");
-    LLMI_REQUIRE(!a.steal || (a.ksplit == 1 && a.steal_tail >= 0 && (a.steal_tail == 0 || a.epi == EPI_ATOMIC)),
-                 "gemv: work stealing needs ksplit 1 (a batch tail only with the atomic epilogue)");
+    LLMI_REQUIRE(a.kpar <= 1 || ((a.kpar == 2 || a.kpar == 4) && (a.epi == EPI_STORE || a.epi == EPI_SILU_MUL) &&
+                                 a.grid == 0 && (a.k / epl) % a.kpar == 0),
+                 "gemv: kpar 2 / 4 needs a store or silu epilogue, an automatic grid and k / kpar whole 16-B chunks");
     LLMI_REQUIRE(a.ldw == 0 || a.ldw >= a.k, "gemv: ldw < k");
     const int grid = gemv_grid(a);
     switch (a.w_dtype) {

@@ -81,12 +81,15 @@ __device__ __forceinline__ float4 gamma4(const void* g, int j) {
 }
 
 // LDS bytes the body needs for a k-wide x: [PK][nc] float4 image + reduction scratch + keys
-__host__ __device__ inline size_t gemv_lds_bytes(int k) { return (size_t)k * 4 + 16 * 4 + kWavesPerBlock * 8; }
+__host__ __device__ inline size_t gemv_lds_bytes(int k) {
+    return (size_t)k * 4 + 16 * 4 + kWavesPerBlock * 8 + kWavesPerBlock * 2 * 4;  // + kpar partials [4][2]
+}
 
 // XPT: float4s of x each thread holds in registers during staging (k <= XPT*4*256);
 // 0 = generic strided staging (standalone only).
 // bid / nblk: this workgroup's index in the GEMV grid and the grid size.
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, typename IO>
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, typename IO,
+          int KPT = 1>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, float4* xs) {
     // residual hand-over (seed_dst <- seed_src slice)
     auto seed = [&, bid0 = bid, nblk0 = nblk]() {
@@ -109,8 +112,21 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
     const int nc = k / EPL;                     // 16-B chunks per row
     float* red = reinterpret_cast<float*>(xs + k4);
     unsigned long long* best_s = reinterpret_cast<unsigned long long*>(red + 16);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float* kpart = reinterpret_cast<float*>(best_s + kWavesPerBlock);  // [wave][ROWS] kpar partial dots
+    const int tid = threadIdx.x, lane = tid & 63;
     const int n_groups = (EPI == EPI_SILU_MUL) ? a.pair_off : (a.n_rows + ROWS - 1) / ROWS;
+    // LLMI_I8_PIPE: bit EPI enables the software-pipelined int8 stream for that epilogue
+    // (4 = gate_up only); LLMI_GEMV_PIPE16 the same for fp16 (both off by default)
+    constexpr bool PIPE = (sizeof(WT) == 1 && kUnroll <= 5 && ((LLMI_I8_PIPE >> EPI) & 1))
+                          || (sizeof(WT) == 2 && ((LLMI_GEMV_PIPE16 >> EPI) & 1));
+    // KPT (GemvArgs::kpar, a template argument so the KPT = 1 kernels are unchanged):
+    // wave w takes K part w % KP of the workgroup's group slot w / KP
+    constexpr bool KPOK = (EPI == EPI_STORE || EPI == EPI_SILU_MUL) && ROWS <= 2 && !PIPE;
+    constexpr int KP = KPOK ? KPT : 1;
+    const int wave = (tid >> 6) / KP, kq = (tid >> 6) % KP;  // group slot and K part
+    constexpr int gpw = kWavesPerBlock / KP;                  // groups per workgroup
+    const int c_lo = KP > 1 ? kq * (nc / KP) : 0;              // this wave's chunks [c_lo, c_hi)
+    const int c_hi = KP > 1 ? c_lo + nc / KP : nc;
     const size_t row_bytes = (size_t)(a.ldw ? a.ldw : a.k) * sizeof(WT);
     const char* wbase = reinterpret_cast<const char*>(a.w) + (size_t)ks * k * sizeof(WT);
     const float4* x4 = reinterpret_cast<const float4*>(a.x + (size_t)ks * k);
@@ -127,11 +143,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int c = base + u * kWave + lane;
-            const int cc = c < nc ? c : nc - 1;
+            const int cc = c < c_hi ? c : c_hi - 1;
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) {
                 const int rr = rows[r] < a.n_rows ? rows[r] : a.n_rows - 1;
-                const unsigned m = (c < nc && rows[r] < a.n_rows) ? 0xFFFFFFFFu : 0u;
+                const unsigned m = (c < c_hi && rows[r] < a.n_rows) ? 0xFFFFFFFFu : 0u;
                 uint4 v = ld_nt16(wbase + (size_t)rr * row_bytes + (size_t)cc * 16);
                 v.x &= m; v.y &= m; v.z &= m; v.w &= m;
                 wv[r][u] = v;
@@ -142,23 +158,16 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int c = base + u * kWave + lane;
-            const float4* xp = xs + (c < nc ? c : nc - 1);  // masked chunks have zero weights
+            const float4* xp = xs + (c < c_hi ? c : c_hi - 1);  // masked chunks have zero weights
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) acc[r] += dot_packet(wv[r][u], xp, nc, (WT*)nullptr);
         }
     };
 
-    // tail work stealing: this workgroup's first ticket, requested before anything else so
-    // its round trip overlaps the static part (see the dynamic part below)
-    const int NS = min(kStealShards, max(1, nblk / 8));
-    const int sh = (bid >> 3) % NS;
-    unsigned first_ticket = 0;
-    if (a.steal != nullptr && tid == 0)
-        first_ticket = __hip_atomic_fetch_add(a.steal + sh * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- prologue. Issue order matters: vmcnt retires loads in issue order, so x
     // (and gamma) go first, then this wave's first weight batch; the weight stream is
     // then in flight while x is staged and the norm is reduced.
-    const int g0 = bid * kWavesPerBlock + wave;
+    const int g0 = bid * gpw + wave;
     int rows0[ROWS];
     rows_of(g0, rows0);
     uint4 w0[ROWS][kUnroll];
@@ -180,7 +189,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
             }
             if (NORM) gv[i] = gamma4<GT>(a.gamma, j);
         }
-        load_batch(w0, rows0, 0);
+        load_batch(w0, rows0, c_lo);
         // RMSNorm (modeling_llama.py:112-117) as gamma*x staged + one scalar rsqrt per
         // dot product in the epilogue: sum_k W[r,k] gamma_k x_k * rstd.
 #pragma unroll
@@ -219,7 +228,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
             }
             xs[(j % PK) * nc + j / PK] = v;
         }
-        load_batch(w0, rows0, 0);
+        load_batch(w0, rows0, c_lo);
     }
     seed();
     float rstd = 1.f;
@@ -232,10 +241,27 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
 
     unsigned long long best = 0ull;
     auto finish = [&](int g, const int* rows, float* acc) {
+        if constexpr (KP > 1) {  // the K parts of one group meet in LDS; part 0 adds them in order
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-            acc[r] = wave_sum(acc[r]) * rstd;
-            if (a.scales != nullptr && rows[r] < a.n_rows) acc[r] *= __half2float(a.scales[rows[r]]);
+            for (int r = 0; r < ROWS; ++r) acc[r] = wave_sum(acc[r]);
+            if (lane == 0)
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) kpart[(tid >> 6) * 2 + r] = acc[r];
+            __syncthreads();
+            if (kq != 0 || g >= n_groups) return;
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                float sum = kpart[(wave * KP) * 2 + r];
+                for (int q = 1; q < KP; ++q) sum += kpart[(wave * KP + q) * 2 + r];
+                acc[r] = sum * rstd;
+                if (a.scales != nullptr && rows[r] < a.n_rows) acc[r] *= __half2float(a.scales[rows[r]]);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                acc[r] = wave_sum(acc[r]) * rstd;
+                if (a.scales != nullptr && rows[r] < a.n_rows) acc[r] *= __half2float(a.scales[rows[r]]);
+            }
         }
         if (EPI == EPI_SILU_MUL) {
             if (lane == 0) IO::st(a.y + g, silu(acc[0]) * acc[1]);
@@ -266,9 +292,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
     // item's loads are issued before the current item's convert + FMA work, across
     // row-group boundaries too; two register buffers, manually unrolled by 2. The
     // item after the last one re-loads the last item (a cache hit, never used).
-    // LLMI_I8_PIPE: bit EPI enables it for that epilogue (4 = gate_up only)
-    constexpr bool PIPE = (sizeof(WT) == 1 && kUnroll <= 5 && ((LLMI_I8_PIPE >> EPI) & 1))
-                          || (sizeof(WT) == 2 && ((LLMI_GEMV_PIPE16 >> EPI) & 1));
+    // (PIPE is defined at the top of the body.)
     if constexpr (PIPE) {
         constexpr int B = kWave * kUnroll;
         const int stride = nblk * kWavesPerBlock;
@@ -318,73 +342,21 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
         }
     }
     constexpr int B = kWave * kUnroll;  // chunks per batch
-    // tail work stealing (GemvArgs::steal): the static part is each wave's first group only
-    // (EPI_ATOMIC: without its last steal_tail batches); see the dynamic part below
-    const bool steal = !PIPE && a.steal != nullptr;
-    const int nbatch = (nc + B - 1) / B;
-    const int tailb = (steal && EPI == EPI_ATOMIC) ? min(a.steal_tail, nbatch - 1) : 0;
-    const int nc_static = (nbatch - tailb) * B;
     // ---- first group (its first batch is already in flight)
-    if (!PIPE && g0 < n_groups) {
+    if (!PIPE && (g0 < n_groups || KP > 1)) {  // kpar: every wave reaches finish's barrier
         float acc[ROWS];
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
-        dot_batch(w0, 0, acc);
-        for (int base = B; base < nc_static; base += B) {
+        dot_batch(w0, c_lo, acc);
+        for (int base = c_lo + B; base < c_hi; base += B) {
             uint4 wv[ROWS][kUnroll];
             load_batch(wv, rows0, base);
             dot_batch(wv, base, acc);
         }
         finish(g0, rows0, acc);
     }
-    if (steal) {
-        // Dynamic units of one workgroup (a group per wave): EPI_ATOMIC with a tail, unit u =
-        // the last tailb batches of groups 4u .. 4u + 3 (the partial sums are exact int64 adds,
-        // so who adds them does not matter); otherwise unit u = groups W + 4u .. W + 4u + 3.
-        // Tickets: shard (bid / 8) % S is shared by 8 consecutive workgroups, one per XCD;
-        // it owns units s, s + S, ... One ticket per unit plus one past the end per workgroup,
-        // prefetched a unit ahead; the shard's last workgroup to leave re-zeroes it.
-        const int W = nblk * kWavesPerBlock;
-        const int ngs = tailb ? min(n_groups, W) : max(n_groups - W, 0);
-        const int U = (ngs + kWavesPerBlock - 1) / kWavesPerBlock;
-        unsigned* tick = a.steal + sh * 32;
-        unsigned* left = a.steal + (kStealShards + sh) * 32;
-        __shared__ unsigned tick_s;
-        auto take = [&]() { return __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-        unsigned t = first_ticket;  // taken at the kernel start
-        for (;;) {
-            if (tid == 0) tick_s = t;
-            __syncthreads();
-            const int u = sh + NS * (int)tick_s;
-            __syncthreads();  // tick_s read by every wave before thread 0 may overwrite it
-            if (u >= U) break;
-            if (tid == 0) t = take();  // the next unit's ticket, in flight during this one
-            const int g = (tailb ? 0 : W) + u * kWavesPerBlock + wave;
-            if (g < n_groups && (!tailb || g < W)) {
-                int rows[ROWS];
-                rows_of(g, rows);
-                float acc[ROWS];
-#pragma unroll
-                for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
-                for (int base = tailb ? nc_static : 0; base < nc; base += B) {
-                    uint4 wv[ROWS][kUnroll];
-                    load_batch(wv, rows, base);
-                    dot_batch(wv, base, acc);
-                }
-                finish(g, rows, acc);
-            }
-        }
-        if (tid == 0) {
-            int members = 0;  // workgroups of this shard: groups of 8 k = sh, sh + NS, ...
-            for (int k = sh; k * 8 < nblk; k += NS) members += min(8, nblk - k * 8);
-            if (__hip_atomic_fetch_add(left, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)members - 1) {
-                __hip_atomic_store(tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(left, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-    // ---- remaining groups (no stealing: every wave's later groups, statically)
-    for (int g = g0 + nblk * kWavesPerBlock; !PIPE && !steal && g < n_groups; g += nblk * kWavesPerBlock) {
+    // ---- remaining groups (KP == 1: a wave's later groups)
+    for (int g = g0 + nblk * kWavesPerBlock; !PIPE && KP == 1 && g < n_groups; g += nblk * kWavesPerBlock) {
         int rows[ROWS];
         rows_of(g, rows);
         float acc[ROWS];

@@ -21,13 +21,13 @@ namespace gemv_detail {
 #endif
 template <typename WT> constexpr int min_waves() { return sizeof(WT) == 1 ? LLMI_GEMV_MIN_WAVES_I8 : LLMI_GEMV_MIN_WAVES; }
 
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX>
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, int KPT = 1>
 __global__ __launch_bounds__(kThreads, min_waves<WT>()) void gemv_kernel(GemvArgs a) {
     // all LDS in one 16-B aligned dynamic region (cdna_hip_programming.md G17):
     // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
     WgStamp ts(a.stamps);
-    gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO>(a, blockIdx.x, gridDim.x, xs);
+    gemv_body<WT, ROWS, EPI, NORM, GT, XPT, kUnroll, XFIX, PlainIO, KPT>(a, blockIdx.x, gridDim.x, xs);
     if constexpr (EPI == EPI_ATOMIC || EPI == EPI_ARGMAX) {  // TP: push yacc / the argmax keys from this launch
         const int k4 = (EPI == EPI_ATOMIC ? a.k / a.ksplit : a.k) / 4;
         xchg_detail::xchg_tail(a.xt, a.xt_cnt, reinterpret_cast<int*>(xs + k4) + 15);  // red[15]: free by now
@@ -46,14 +46,14 @@ inline int device_cus() {
     }
     return cus;
 }
-template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int U, bool XF>
+template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int U, bool XF, int KPT = 1>
 int launch_k(const GemvArgs& a, int grid, size_t lds, hipStream_t s) {
-    auto kern = gemv_kernel<WT, ROWS, EPI, NORM, GT, XPT, U, XF>;
+    auto kern = gemv_kernel<WT, ROWS, EPI, NORM, GT, XPT, U, XF, KPT>;
     // An automatic grid larger than what is resident leaves the excess workgroups to
     // start only when early ones retire -- a second, latency-bound round at the tail
     // (profiles/r01c: int8 13B q/k/v and down). Clamp it to the resident count
     // (argmax grids stay: their partial count is fixed by gemv_grid for step_start).
-    if (EPI != EPI_ARGMAX && a.grid == 0) {
+    if (EPI != EPI_ARGMAX && a.grid == 0 && a.kpar <= 1) {  // (kpar: one group per wave, no loop: never clamped)
         static size_t occ_lds = ~(size_t)0;
         static int occ_blocks = 0;
         if (lds != occ_lds) {
@@ -77,6 +77,19 @@ int launch_u(const GemvArgs& a, int grid, hipStream_t s) {
     const int kl = (EPI == EPI_ATOMIC) ? a.k / a.ksplit : a.k;  // x extent one workgroup stages
     const size_t lds = gemv_lds_bytes(kl);
     const int k4 = kl / 4;
+    if constexpr ((EPI == EPI_STORE || EPI == EPI_SILU_MUL) && NORM && XF && U == 4) {
+        // kpar (a TP rank's q/k/v and gate_up): the engine's normed fixed-point projections,
+        // hidden <= 5120
+        if (a.kpar > 1) {
+            LLMI_REQUIRE(k4 <= 5 * kThreads, "gemv: kpar needs k <= 5120");
+            if (a.kpar == 2)
+                return k4 <= 4 * kThreads ? launch_k<WT, ROWS, EPI, NORM, GT, 4, U, XF, 2>(a, grid, lds, s)
+                                          : launch_k<WT, ROWS, EPI, NORM, GT, 5, U, XF, 2>(a, grid, lds, s);
+            return k4 <= 4 * kThreads ? launch_k<WT, ROWS, EPI, NORM, GT, 4, U, XF, 4>(a, grid, lds, s)
+                                      : launch_k<WT, ROWS, EPI, NORM, GT, 5, U, XF, 4>(a, grid, lds, s);
+        }
+    }
+    LLMI_REQUIRE(a.kpar <= 1, "gemv: kpar only for the engine's normed fixed-point q/k/v and gate_up");
     if (k4 <= 4 * kThreads) return launch_k<WT, ROWS, EPI, NORM, GT, 4, U, XF>(a, grid, lds, s);
     if (k4 <= 5 * kThreads) return launch_k<WT, ROWS, EPI, NORM, GT, 5, U, XF>(a, grid, lds, s);    // 13B hidden
     if (k4 <= 11 * kThreads) return launch_k<WT, ROWS, EPI, NORM, GT, 11, U, XF>(a, grid, lds, s);  // 7B inter
@@ -97,9 +110,10 @@ int launch_u(const GemvArgs& a, int grid, hipStream_t s) {
 template <typename WT, int EPI>
 int pick_unroll(const GemvArgs& a, int groups) {
     const int kl = (EPI == EPI_ATOMIC) ? a.k / a.ksplit : a.k;
-    const int nc = kl / WT_<WT>::EPL;
+    const int nc = kl / WT_<WT>::EPL / (a.kpar > 1 ? a.kpar : 1);  // chunks one wave streams
     auto slots = [&](int u) { const int b = kWave * u; return (nc + b - 1) / b * b; };
     int best = (EPI != EPI_ARGMAX && groups >= 4096 && groups <= 12288 && kUnrollMax >= 4) ? 4 : kUnrollMax;
+    if (a.kpar > 1) best = 4;  // a K part is <= 2 batches of 4: fewest masked slots of {4, 5, 8}
     for (int u : {4, 5, 8})
         if (u <= kUnrollMax && slots(u) < slots(best)) best = u;
     return best;

@@ -72,17 +72,14 @@ struct GemvArgs {
     // xt.buf null = off; xt_cnt = the engine's arrival counter pair (xchg_impl.h xchg_tail)
     XchgArgs xt;
     unsigned* xt_cnt = nullptr;
-    // tail work stealing (gemv_impl.h): each wave keeps its first row group (for EPI_ATOMIC
-    // without its last steal_tail batches); the rest -- row groups beyond the first wave
-    // round, or those last batches -- go out as workgroup-sized units from kStealShards
-    // ticket counters, each shared by one workgroup of every XCD, so whichever XCD the
-    // memory system serves first takes more. steal: [2][kStealShards][32] words (tickets,
-    // then arrivals), zero at launch and left zero (a shard's last workgroup resets it).
-    unsigned* steal = nullptr;
-    int steal_tail = 0;
+    // K split INSIDE a workgroup (small shards, e.g. a TP-8 rank's q/k/v and gate_up, whose
+    // 192 / 344 four-wave workgroups leave CUs idle or doubled): kpar waves (2 or 4) share one
+    // row group, each streaming 1/kpar of K; their partial dots meet in LDS and the first
+    // adds them in order. Grid = ceil(groups / (4 / kpar)), every wave exactly one group.
+    // EPI_STORE / EPI_SILU_MUL only; 0 / 1 = off.
+    int kpar = 0;
 };
-constexpr int kStealShards = 64;
-constexpr int kStealWords = 2 * kStealShards * 32;
+
 
 int gemv_launch(const GemvArgs& a, hipStream_t s);
 int gemv_grid(const GemvArgs& a);  // blocks gemv_launch will use

@@ -151,7 +151,7 @@ class Engine:
         call("llmi_engine_xchg_open", self._h, buf)
 
     def set_option(self, name: str, value: int):
-        """llmi_engine_set_option: tuning switches for same-process A/B ("steal": 0..3)."""
+        """llmi_engine_set_option: tuning switches for same-process A/B ("kpar": 0 / 1)."""
         call("llmi_engine_set_option", self._h, name.encode(), int(value))
 
     def xchg_loopback(self):

@@ -205,33 +205,27 @@ def test_host_device_position_mismatch_is_reported(use_graph):
             e.tokens()
 
 
-@pytest.mark.parametrize("steal", [1, 2, 3])
-def test_gemv_work_stealing_matches_fixture_and_is_repeatable(steal):
-    """GEMV tail work stealing (llmi_engine_set_option "steal"): q/k/v and gate_up hand their
-    row groups past the first wave round to whichever workgroup asks first (each group still
-    computed whole by one wave: bitwise the static result), down hands out the last batch of
-    every row pair (its partial sums added as exact int64: deterministic, a different fp32
-    association from the static kernel). F3: tokens exact, logits within 1e-3 of the reference;
-    graph replay equals eager launches bitwise, across split-count boundaries; mode 1 is
-    bitwise the static kernels."""
-    f = load("f3_decode.npz")
-    cfg = preset("llama2-7b", layers=2, max_seq=160)
-    cfg.kv_dtype = _lib.F32
+@pytest.mark.parametrize("world", [4, 8])
+def test_kpar_small_shard_gemv_matches_unsplit(world):
+    """K split inside the workgroup (GemvArgs::kpar) for a TP rank's q/k/v and gate_up: 2 or 4
+    waves share a row group, their partial dots added in order. Against the unsplit kernels
+    (llmi_engine_set_option "kpar" 0) on the same looped-back rank: tokens equal, logits within
+    fp32 reassociation (1e-5); graph replay equals eager launches bitwise."""
+    cfg = preset("llama2-7b", layers=2, max_seq=160, tp_rank=0, tp_world=world)
+    prompt = np.array([1, 5, 9, 13, 17, 21, 25, 29], np.int32)
     out = {}
     with Engine(cfg) as e:
-        e.load_synthetic(int(f["seed"]))
-        for st in (0, steal):
-            e.set_option("steal", st)
+        e.load_synthetic(3)
+        e.xchg_loopback()
+        e.set_exchange(1)
+        for kp in (0, 1):
+            e.set_option("kpar", kp)
             for g in (True, False):
-                toks = e.generate(f["prompt"], 140, use_graph=g)
-                out[(st, g)] = (toks.copy(), e.logits().copy())
-    np.testing.assert_array_equal(out[(steal, True)][0][:len(f["tokens"])], f["tokens"])
-    np.testing.assert_array_equal(out[(steal, True)][0], out[(0, True)][0])
-    np.testing.assert_array_equal(out[(steal, True)][1], out[(steal, False)][1])
-    np.testing.assert_array_equal(out[(steal, True)][0], out[(steal, False)][0])
-    r = rel(out[(steal, True)][1], out[(0, True)][1])
-    print(f"steal {steal}: logits rel-L2 vs static {r:.2e}")
-    if steal == 1:
-        assert r == 0.0
-    else:
-        assert r < 1e-5
+                toks = e.generate(prompt, 70, use_graph=g)
+                out[(kp, g)] = (toks.copy(), e.logits().copy())
+    np.testing.assert_array_equal(out[(1, True)][0], out[(0, True)][0])
+    np.testing.assert_array_equal(out[(1, True)][0], out[(1, False)][0])
+    np.testing.assert_array_equal(out[(1, True)][1], out[(1, False)][1])
+    r = rel(out[(1, True)][1], out[(0, True)][1])
+    print(f"kpar on vs off, TP {world}: logits rel-L2 {r:.2e}")
+    assert r < 1e-5

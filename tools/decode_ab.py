@@ -3,7 +3,7 @@
 ids, graph-replayed forwards at positions 0..max_seq-1), alternating the variants pass by pass
 so box drift hits all of them alike.
 
-    python tools/decode_ab.py --option steal --values 0,3 [--passes 3] [--layers 32] [--max-seq 2048]
+    python tools/decode_ab.py --option kpar --values 0,1 [--tp-world 8] [--passes 3] [--layers 32] [--max-seq 2048]
 
 One JSON line per (pass, value): us per token and tok/s (generated tokens as bench.py counts them).
 """
@@ -22,15 +22,17 @@ from llmi.engine import Engine, preset, synth_prompt  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--option", default="steal")
-    ap.add_argument("--values", default="0,3")
+    ap.add_argument("--option", default="kpar")
+    ap.add_argument("--values", default="0,1")
+    ap.add_argument("--tp-world", type=int, default=1, help="> 1: rank 0, exchange looped back (mode --exchange)")
+    ap.add_argument("--exchange", type=int, default=1)
     ap.add_argument("--passes", type=int, default=3)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--max-seq", type=int, default=2048)
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--int8", action="store_true")
     a = ap.parse_args()
-    cfg = preset(a.preset, layers=a.layers, max_seq=a.max_seq)
+    cfg = preset(a.preset, layers=a.layers, max_seq=a.max_seq, tp_rank=0, tp_world=a.tp_world)
     cfg.kv_dtype = llmi.F16
     if a.int8:
         cfg.weight_dtype = llmi.I8
@@ -38,6 +40,9 @@ def main():
     prompt = synth_prompt(0, 8, cfg.vocab)
     with Engine(cfg) as e:
         e.load_synthetic(0)
+        if a.tp_world > 1:
+            e.xchg_loopback()
+            e.set_exchange(a.exchange)
         toks = {}
         for v in vals:  # capture + warm every variant once
             e.set_option(a.option, v)

@@ -58,12 +58,15 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--out", default="")
+    ap.add_argument("--tp-world", type=int, default=1,
+                    help="> 1: rank 0 of that TP degree, exchange looped back (llmi_engine_xchg_loopback)")
+    ap.add_argument("--exchange", type=int, default=0, help="with --tp-world: exchange mode 0 / 1 / 2")
     ap.add_argument("--wg-layer", type=int, default=-1,
                     help="also dump layer L's per-workgroup {start, end, xcd, cu} for q/k/v, o and down, "
                          "with completion quantiles per XCD (VERDICT r04 item 3a)")
     a = ap.parse_args()
     lib = _lib.lib()
-    cfg = preset(a.preset, layers=a.layers, max_seq=2048)
+    cfg = preset(a.preset, layers=a.layers, max_seq=2048, tp_rank=0, tp_world=a.tp_world)
     n_slots = 5 * a.layers + 1
     stride = slot_wgs(cfg)
     nbytes = n_slots * stride * 64
@@ -74,6 +77,9 @@ def main():
            "mode": "hipGraph replay (one captured graph per active split count)", "ctx": {}}
     with Engine(cfg) as e:
         e.load_synthetic(0)
+        if a.tp_world > 1:
+            e.xchg_loopback()
+            e.set_exchange(a.exchange)
         e.set_prompt(synth_prompt(0, 8, cfg.vocab))
         _lib.call("llmi_engine_debug_timeline", e._h, buf, C.c_size_t(nbytes), stride)
         pos = 0
