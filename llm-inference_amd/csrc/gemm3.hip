@@ -46,6 +46,7 @@
 // Roofline: MFMA (fp16 dense 2.5 PFLOP/s); FLOPs per launch 2 * M * N * K * planes.
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -53,6 +54,12 @@
 
 #ifndef LLMI_G3_PIN8
 #define LLMI_G3_PIN8 1  // 0: let the compiler place the fp8 lo MFMAs (A/B builds only)
+#endif
+#ifndef LLMI_G3_VM2
+#define LLMI_G3_VM2 1  // counted vmcnt only in j1 and j3 (0: in every phase; A/B builds only)
+#endif
+#ifndef LLMI_G3_BFIRST
+#define LLMI_G3_BFIRST 1  // j0 reads B0 before A0, a scheduling barrier between (0: A first; A/B builds only)
 #endif
 
 namespace llmi {
@@ -232,7 +239,10 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
     // prologue: virtual phases -6 .. -1 = A0, B0, B1, A1 of tile 0, A0, B0 of tile 1
     issue(0, 0); issue(0, 2); issue(0, 3); issue(0, 1);
     issue(1, 0); issue(1, 2);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0 of tile 0
+    if (LLMI_G3_VM2)  // A0, B0, B1 of tile 0 (j0 has no wait of its own; A1 is retired by j1's)
+        wait_vm(2 * (min(1, KT - 1) * 2 + 1));
+    else
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0 of tile 0
     bar();
     if (wr == 1) bar();  // ping-pong: group 1 one barrier behind
 
@@ -241,27 +251,43 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
         const char* buf = lds + (kt & 1) * kBuf;
         const int n = 4 * kt;
         // j0: quadrant (A0, B0)
-        read_a(buf);
-        read_b(buf + 2 * kHalf, b0);
+        if (LLMI_G3_BFIRST) {
+            read_b(buf + 2 * kHalf, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            read_a(buf);
+        } else {
+            read_a(buf);
+            read_b(buf + 2 * kHalf, b0);
+        }
         issue(kt + 1, 3);
-        sync_reads(n);
+        if (LLMI_G3_VM2) bar(); else sync_reads(n);
         if constexpr (F8) mma8(acc[0][0], b0); else mma(acc[0][0], b0);
         bar();
         // j1: quadrant (A0, B1)
         read_b(buf + 3 * kHalf, b1);
         issue(kt + 1, 1);
-        sync_reads(n + 1);
+        if (LLMI_G3_VM2) {  // retires A1 of tile kt (read in j2): 4 half-images issued after it
+            wait_vm(vm_count(n + 1));
+            bar();
+        } else {
+            sync_reads(n + 1);
+        }
         if constexpr (F8) mma8(acc[0][1], b1); else mma(acc[0][1], b1);
         bar();
         // j2: quadrant (A1, B1)
         read_a(buf + kHalf);
         issue(kt + 2, 0);
-        sync_reads(n + 2);
+        if (LLMI_G3_VM2) bar(); else sync_reads(n + 2);
         if constexpr (F8) mma8(acc[1][1], b1); else mma(acc[1][1], b1);
         bar();
         // j3: quadrant (A1, B0)
         issue(kt + 2, 2);
-        sync_reads(n + 3);
+        if (LLMI_G3_VM2) {  // retires A0 / B0 and B1 of tile kt + 1 (read in its j0 / j1): 3 issued after B1
+            wait_vm(2 * max(0, min(n + 3, n_last) - n));
+            bar();
+        } else {
+            sync_reads(n + 3);
+        }
         if constexpr (F8) mma8(acc[1][0], b0); else mma(acc[1][0], b0);
         bar();
     };

@@ -120,7 +120,11 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&slab, maxY * 4));
     CK(hipMalloc(&yh, maxY * 2));
     CK(hipMalloc(&yl, maxY * 2));
-    if (exact_data) {  // hi = 0, lo = j / 4096, W = j / 64: the lo8 pass is then exact (fp32 sums of integers)
+    if (exact_data == 2) {  // zero-filled operands: the kernel's schedule without the power draw of random bits
+        CK(hipMemset(ah, 0, maxA * 2));
+        CK(hipMemset(al, 0, maxA * 2));
+        CK(hipMemset(w, 0, maxW * 2));
+    } else if (exact_data) {  // hi = 0, lo = j / 4096, W = j / 64: the lo8 pass is then exact (fp32 sums of integers)
         CK(hipMemset(ah, 0, maxA * 2));
         hipLaunchKernelGGL(fill_int_kernel, dim3(2048), dim3(256), 0, 0, al, maxA, 2u, 4096.f);
         hipLaunchKernelGGL(fill_int_kernel, dim3(2048), dim3(256), 0, 0, w, maxW, 3u, 64.f);

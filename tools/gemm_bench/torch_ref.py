@@ -12,10 +12,17 @@ def main():
     m = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     shapes = [("qkv", 12288, 4096), ("o", 4096, 4096), ("gate_up", 22016, 4096), ("down", 4096, 11008),
               ("sq4096", 4096, 4096)]
-    for name, n, k in shapes:
+    variants = [("randn", torch.float16)]
+    if len(sys.argv) > 2 and sys.argv[2] == "all":  # + zero-filled fp16 and random bf16 (power vs schedule)
+        variants += [("zeros", torch.float16), ("randn", torch.bfloat16)]
+    for (name, n, k), (data, dt) in [(s, v) for s in shapes for v in variants]:
         mm = 4096 if name == "sq4096" else m
-        a = torch.randn(mm, k, device="cuda", dtype=torch.float16)
-        w = torch.randn(n, k, device="cuda", dtype=torch.float16) * 0.05
+        if data == "zeros":
+            a = torch.zeros(mm, k, device="cuda", dtype=dt)
+            w = torch.zeros(n, k, device="cuda", dtype=dt)
+        else:
+            a = torch.randn(mm, k, device="cuda", dtype=dt)
+            w = torch.randn(n, k, device="cuda", dtype=dt) * 0.05
         for _ in range(3):
             torch.matmul(a, w.t())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -26,7 +33,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / iters
-        print(json.dumps({"shape": name, "m": mm, "n": n, "k": k, "torch_us": round(us, 2),
+        print(json.dumps({"shape": name, "data": data, "dtype": str(dt), "m": mm, "n": n, "k": k, "torch_us": round(us, 2),
                           "torch_tflops": round(2.0 * mm * n * k / us * 1e-6, 1)}), flush=True)
 
 
