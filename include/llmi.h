@@ -142,6 +142,12 @@ int llmi_stream_errors(llmi_stream_t stream, int* flags);
  * must still be correct: flags carry a per-launch epoch). 0 / launches 0 clears it. */
 int llmi_debug_stream_k(int mode, int launches);
 
+/* Diagnostics (no reference counterpart): while `stamps` (device memory, 8 u64 per
+ * workgroup) is non-null, every launch of the transposed prefill attention kernel writes its
+ * per-workgroup timeline there (WgStamp: start, copies of the first block landed, loop end,
+ * end, __smid(), then query block | head << 16, key blocks). Null turns it off. */
+int llmi_debug_prefill_stamps(void* stamps);
+
 /* One decode row through the HBM-streaming GEMV with its fused prologue/epilogue -- what
  * LlamaSelfDecoder::forward strings together for a token (self_decoder.cpp:59-81 fused):
  *   gamma != NULL: x is RMS-normalised and scaled by gamma (dtype gamma_dtype) first;

@@ -114,6 +114,11 @@ int llmi_debug_stream_k(int mode, int launches) {
     return LLMI_OK;
 }
 
+int llmi_debug_prefill_stamps(void* stamps) {
+    prefill_stamps_debug(static_cast<unsigned long long*>(stamps));
+    return LLMI_OK;
+}
+
 int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
                 llmi_stream_t stream) {
     LLMI_REQUIRE(m >= 1 && n >= 1 && k >= 1, "linear: m, n, k must be >= 1");

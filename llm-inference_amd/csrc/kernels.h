@@ -160,6 +160,7 @@ struct Gemm2Args {
 constexpr int kSkCtlWords = 64;    // stream-K control words ahead of the flags (256 B)
 // the next `launches` stream-K launches run with sk_test = mode (llmi_debug_stream_k)
 void gemm3_sk_debug(int mode, int launches);
+void prefill_stamps_debug(unsigned long long* stamps);  // llmi_debug_prefill_stamps
 // stream-K plan for gemm3 (m rows, n columns -- gate_up: 2 x inter --, k, planes / lo8 as in
 // Gemm2Args) on g workgroups: slots per tile (0: stream-K does not apply), and the bytes of
 // partial slots and of flags it needs

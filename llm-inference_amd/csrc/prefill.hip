@@ -17,8 +17,10 @@
 // d * M^2 / 2), bound by LDS operand traffic in this fp32 form; the GEMMs
 // around it dominate prefill (gemm.hip).
 #include <algorithm>
+#include <atomic>
 
 #include <cstdlib>
+#include <string>
 
 #include "kernels.h"
 
@@ -523,12 +525,313 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float
     }
 }
 
+// ---- Transposed form (round 5). Workgroup = (64 query rows, head, key chunk) as in
+// attn_prefill_mfma_kernel, but 8 waves: wave w owns query rows 16 (w & 3) .. + 15 and the
+// key HALF kp = w >> 2 (keys 32 kp .. 32 kp + 31) of every 64-key block, with its own online
+// softmax state; the two halves are combined once, in LDS, at the end. The two products are
+// oriented so that neither P nor V needs an LDS rewrite:
+//   S^T = K Q^T   A = K rows from the LDS image, B = the Q fragments: the accumulator holds
+//                 ONE query per lane (column lane & 15) and 8 keys, so a softmax row
+//                 reduction is 7 register ops + 2 cross-group shuffles;
+//   O^T = V^T P^T B = P^T straight from the S^T accumulators (the two 16-key tiles of the
+//                 wave's half, converted to fp16 planes in registers), A = V^T read from a
+//                 ROW-major V image with ds_read_b64_tr_b16 (the hardware transpose).
+// K and V are copied HBM -> LDS by global_load_lds_dwordx4 (no register staging) through a
+// ring of kStages 32-KB stages, kStages - 1 blocks in flight ahead of the one computed:
+// the kernel was DMA-latency-bound with one block of look-ahead (r05p: 22.2 us / layer
+// without key chunks, 2.7 us per block on the critical path). The swizzles are applied by
+// permuting each lane's SOURCE chunk (the DMA writes lane-linear 1 KB spans).
+// Key order inside a 16-key tile: the A-operand lane of row i reads key kperm(i) =
+// 4 ksig(i >> 2) + (i & 3) (ksig = 0 2 1 3), so accumulator group fq holds keys
+// 4 ksig(fq) + r and a transposed read's 32-lane half takes two 4-row blocks 8 rows apart
+// in the V image (conflict-free, guide T10; PMC SQ_LDS_BANK_CONFLICT = 0); the PV k order
+// uses the same map. Scores are kept in log2 units (q pre-scaled by log2(e) / sqrt(d),
+// v_exp_f32 in the softmax); the partial m written for the merge is in those units too.
+typedef short s4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int ksig(int g) { return ((g & 1) << 1) | (g >> 1); }
+// V image: 16-B chunk ch of 256-B row r at chunk ch ^ vtr_swz(r) (guide T10 layout (b))
+__device__ __forceinline__ int vtr_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ s4v tr_read(const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(p));
+}
+// global_load_lds_dwordx4 with a uniform base (SGPRs) and a per-lane 32-bit byte offset:
+// the wave's 64 lanes fill 1 KB of LDS from `lds` on, lane-linear
+__device__ __forceinline__ void pf_glds(const void* sbase, unsigned voff, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds)
+                 : "memory");
+}
+constexpr int kTrThreads = 512;
+constexpr int kStages = 4;
+constexpr int kImg = KB * D * 2;  // one 64-key image (K or V): 16 KB
+
+template <int P>
+__global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float* qkv, int ld, int m_rows, int p0,
+                                                                     int heads, int kv_heads, const __half* k_cache,
+                                                                     const __half* v_cache, int max_seq, float* out,
+                                                                     _Float16* out_hi, _Float16* out_lo, int ldo, int cb,
+                                                                     float* ws, int maxc, int lo8,
+                                                                     unsigned long long* stamps) {
+    __shared__ __attribute__((aligned(16))) char smem[kStages * 2 * kImg];  // [stage][K | V]
+    WgStamp ts(stamps);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int qt = w & 3, kp = w >> 2;  // query tile, key half
+
+    const int nqb = (m_rows + QM - 1) / QM;
+    const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;  // XCD-aware order: attn_prefill_mfma_kernel
+    const int per = (heads - xcd + 7) / 8;
+    int items = 0;
+    for (int q = 0; q < nqb; ++q) items += (pf_nkb(q, p0, m_rows) + cb - 1) / cb;
+    if (r >= per * items) return;
+    const int h = xcd + 8 * (r % per);
+    int qb = nqb - 1, chunk = 0, nch = 1;
+    for (int idx = r / per; qb >= 0; --qb) {
+        nch = (pf_nkb(qb, p0, m_rows) + cb - 1) / cb;
+        if (idx < nch) {
+            chunk = idx;
+            break;
+        }
+        idx -= nch;
+    }
+    const int kvh = h / (heads / kv_heads);
+    const int q_first = qb * QM;
+    const float qscale = 1.4426950408889634f / sqrtf((float)D);  // log2(e) / sqrt(d)
+
+    h8 qa[P][4];
+    float4 qraw[4][2];
+    {
+        const int qrow = min(q_first + 16 * qt + fr, m_rows - 1);
+        const float* qp = qkv + (size_t)qrow * ld + (size_t)h * D;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            qraw[ks][0] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq);
+            qraw[ks][1] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq + 4);
+        }
+    }
+    const int kend = p0 + min(q_first + QM, m_rows);
+    const int nkb = (kend + KB - 1) / KB;
+    const int kb0 = chunk * cb, kb1 = min(kb0 + cb, nkb);
+    const void* kc = k_cache + (size_t)kvh * max_seq * D;
+    const void* vc = v_cache + (size_t)kvh * max_seq * D;
+    const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    // wave w fills 1-KB spans n = 8 i + w (image rows 4 n .. 4 n + 3) of both images: lane ->
+    // row 4 n + lane / 16, physical chunk lane % 16 = logical chunk ^ swizzle. 4 copies per wave
+    auto issue = [&](int kb) {
+        const unsigned sb = lds0 + (unsigned)((kb - kb0) % kStages) * 2 * kImg;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int n = 8 * i + w, row = 4 * n + fq;
+            const unsigned src = (unsigned)min(kb * KB + row, kend - 1) * (unsigned)(D * 2);
+            const unsigned dst = __builtin_amdgcn_readfirstlane(sb + n * 1024);
+            pf_glds(kc, src + ((fr ^ (row & 15)) << 4), dst);
+            pf_glds(vc, src + ((fr ^ vtr_swz(row)) << 4), dst + kImg);
+        }
+    };
+
+    float m_run = -INFINITY, l_run = 0.f;  // this lane's query (column fr), log2 units
+    f4 o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f4{0.f, 0.f, 0.f, 0.f};
+    const int qpos = p0 + q_first + 16 * qt + fr;
+    const int qpos_max = p0 + q_first + 16 * qt + 15;               // the wave's last query
+    const int arow = 32 * kp + 4 * ksig(fr >> 2) + (fr & 3);        // K image row of this A lane (tile 0)
+
+#pragma unroll
+    for (int i = 0; i < kStages - 1; ++i)
+        if (kb0 + i < kb1) issue(kb0 + i);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const float v[8] = {qraw[ks][0].x, qraw[ks][0].y, qraw[ks][0].z, qraw[ks][0].w,
+                            qraw[ks][1].x, qraw[ks][1].y, qraw[ks][1].z, qraw[ks][1].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float x = v[e] * qscale;
+            const _Float16 hi = (_Float16)x;
+            qa[0][ks][e] = hi;
+            if (P == 2) qa[P - 1][ks][e] = (_Float16)(x - (float)hi);
+        }
+    }
+    if (ts.p && t == 0) {
+        ts.p[5] = (unsigned long long)qb | (unsigned long long)h << 16;
+        ts.p[6] = (unsigned long long)(kb1 - kb0);
+    }
+    const int tq = fr >> 2, tp = fr & 3;
+    for (int kb = kb0; kb < kb1; ++kb) {
+        // copies in flight behind block kb: min(kStages - 2, kb1 - 1 - kb) blocks of 4 per wave
+        const int ahead = min(kStages - 2, kb1 - 1 - kb);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's copies of block kb landed; stage of kb - 1 is free
+        if (kb == kb0) ts.mark(1);
+        if (kb + kStages - 1 < kb1) issue(kb + kStages - 1);
+        // a key half entirely past the wave's last query contributes nothing (wave-uniform)
+        if (kb * KB + 32 * kp > qpos_max) continue;
+        const char* Ks = smem + ((kb - kb0) % kStages) * 2 * kImg;
+        const char* Vs = Ks + kImg;
+
+        f4 s[2];
+        s[0] = s[1] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = 16 * j + arow;
+                const h8 ak = *reinterpret_cast<const h8*>(Ks + row * 256 + (((4 * ks + fq) ^ (row & 15)) << 4));
+#pragma unroll
+                for (int p = 0; p < P; ++p) s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ak, qa[p][ks], s[j], 0, 0, 0);
+            }
+        }
+        // s[j][e]: key kb * KB + 32 kp + 16 j + 4 ksig(fq) + e for query qpos. Causal mask
+        // (build_causal_mask.cu:29: key <= query position) only where the half reaches past
+        // the wave's first query or the keys' end (wave-uniform test)
+        const int kbase = kb * KB + 32 * kp;
+        if (kbase + 31 > p0 + q_first + 16 * qt || kbase + 31 >= kend) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int key = kbase + 16 * j + 4 * ksig(fq) + e;
+                    if (key > qpos || key >= kend) s[j][e] = -INFINITY;
+                }
+        }
+        float mx = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                         fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        // a query with every key of the half masked: m stays -inf, p = 0
+        const float m_new = fmaxf(m_run, mx);
+        const float m_use = m_new == -INFINITY ? 0.f : m_new;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+        m_run = m_new;
+        float ps = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float pv = __builtin_amdgcn_exp2f(s[j][e] - m_use);
+                s[j][e] = pv;
+                ps += pv;
+            }
+        ps += __shfl_xor(ps, 16);
+        ps += __shfl_xor(ps, 32);
+        l_run = l_run * alpha + ps;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= alpha;
+
+        // O^T += V^T P^T over the half's 32 keys: P^T element e = s[e / 4][e % 4]; the V^T
+        // fragment's elements 0-3 / 4-7 are the transposed reads of image rows
+        // 32 kp + 4 ksig(fq) + (0..3) and the same + 16, columns 16 dt + fr
+        h8 pb[P];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float x = s[e >> 2][e & 3];
+            const _Float16 hi = (_Float16)x;
+            pb[0][e] = hi;
+            if (P == 2) pb[P - 1][e] = (_Float16)(x - (float)hi);
+        }
+        const int row0 = 32 * kp + 4 * ksig(fq) + tq;  // row0 + 16 has the same swizzle
+        const char* vrow0 = Vs + row0 * 256 + 8 * (tp & 1);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            const int cofs = ((2 * dt + (tp >> 1)) ^ vtr_swz(row0)) << 4;
+            const s4v v0 = tr_read(vrow0 + cofs);
+            const s4v v1 = tr_read(vrow0 + 16 * 256 + cofs);
+            const h8 av = __builtin_bit_cast(h8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+            for (int p = 0; p < P; ++p) o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, pb[p], o[dt], 0, 0, 0);
+        }
+    }
+
+    // epilogue. o[dt][e] = O[query 16 qt + fr][dim 16 dt + 4 fq + e] of this key half.
+    // Half 1 leaves (O, m, l) in LDS; half 0 combines: M = max, a_i = 2^(m_i - M),
+    // L = l_0 a_0 + l_1 a_1, O = O_0 a_0 + O_1 a_1 (/ L for a direct output), into the padded
+    // fp32 image that the 16-B store loop of attn_prefill_mfma_kernel reads.
+    constexpr int kIs = D + 4;
+    __syncthreads();  // every wave is done with the stages (no copy is in flight)
+    ts.mark(2);
+    float* img1 = reinterpret_cast<float*>(smem);   // half 1's O rows [64][kIs]
+    float* ml1 = img1 + QM * kIs;                   // half 1's m, l [2][64]
+    float* img = ml1 + 2 * QM;                      // the combined rows [64][kIs]
+    const int lr = 16 * qt + fr;
+    if (kp == 1) {
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+            *reinterpret_cast<f4*>(img1 + lr * kIs + 16 * dt + 4 * fq) = o[dt];
+        if (fq == 0) {
+            ml1[lr] = m_run;
+            ml1[QM + lr] = l_run;
+        }
+    }
+    __syncthreads();
+    if (kp == 0) {
+        const float m1 = ml1[lr], l1 = ml1[QM + lr];
+        const float M = fmaxf(m_run, m1);
+        const float M_use = M == -INFINITY ? 0.f : M;
+        const float a0 = __builtin_amdgcn_exp2f(m_run - M_use), a1 = __builtin_amdgcn_exp2f(m1 - M_use);
+        const float L = l_run * a0 + l1 * a1;
+        const float sc = nch > 1 ? 1.f : 1.0f / L;
+        const float s0 = a0 * sc, s1 = a1 * sc;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            const f4 o1 = *reinterpret_cast<const f4*>(img1 + lr * kIs + 16 * dt + 4 * fq);
+            *reinterpret_cast<f4*>(img + lr * kIs + 16 * dt + 4 * fq) = o[dt] * s0 + o1 * s1;
+        }
+        if (nch > 1 && fq == 0) {
+            float* part = ws + ((size_t)(h * nqb + qb) * maxc + chunk) * kPartFloats;
+            part[QM * D + lr] = M;
+            part[QM * D + QM + lr] = L;
+        }
+    }
+    __syncthreads();
+    if (nch > 1) {  // partial: unnormalised O rows of this chunk (m, l written above)
+        float* part = ws + ((size_t)(h * nqb + qb) * maxc + chunk) * kPartFloats;
+#pragma unroll
+        for (int i = 0; i < QM * D / 4 / kTrThreads; ++i) {
+            const int f = i * kTrThreads + t, rr = f >> 5, c4 = f & 31;
+            reinterpret_cast<float4*>(part)[f] = *reinterpret_cast<const float4*>(img + rr * kIs + 4 * c4);
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < QM * D / 8 / kTrThreads; ++i) {
+        const int f = i * kTrThreads + t, rr = f >> 4, c8 = f & 15;
+        const int row = q_first + rr;
+        if (row >= m_rows) continue;
+        const float4 x0 = *reinterpret_cast<const float4*>(img + rr * kIs + 8 * c8);
+        const float4 x1 = *reinterpret_cast<const float4*>(img + rr * kIs + 8 * c8 + 4);
+        const size_t idx = (size_t)row * ldo + (size_t)h * D + 8 * c8;
+        if (out_hi) {
+            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            h8 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                hv[e] = (_Float16)v[e];
+                lv[e] = (_Float16)(v[e] - (float)hv[e]);
+            }
+            *reinterpret_cast<h8*>(out_hi + idx) = hv;
+            if (out_lo && lo8)
+                *reinterpret_cast<uint2*>(reinterpret_cast<char*>(out_lo + (size_t)row * ldo) + (size_t)h * D + 8 * c8) =
+                    make_uint2(lo8_pack4(v[0] - (float)hv[0], v[1] - (float)hv[1], v[2] - (float)hv[2], v[3] - (float)hv[3]),
+                               lo8_pack4(v[4] - (float)hv[4], v[5] - (float)hv[5], v[6] - (float)hv[6], v[7] - (float)hv[7]));
+            else if (out_lo)
+                *reinterpret_cast<h8*>(out_lo + idx) = lv;
+        } else {
+            *reinterpret_cast<float4*>(out + idx) = x0;
+            *reinterpret_cast<float4*>(out + idx + 4) = x1;
+        }
+    }
+}
+
 // grid (nqb, heads), block 256: the chunks of a split query block, combined in chunk
 // order: M = max m_c, L = sum l_c e^(m_c - M), O = sum O_c e^(m_c - M) / L. Four passes
 // of 16 rows; thread t: row 16 pass + t / 16, dims 8 (t % 16) .. + 8, so 16 lanes cover a
 // row with 16-B loads and stores. Every chunk's loads are issued before any is used
 // (MAXC slots, clamped chunk index, unused slots weighted 0): one memory round trip.
-template <int MAXC>
+template <int MAXC, bool L2>  // L2: the partials' m are in log2 units (attn_prefill_tr_kernel)
 __global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const float* ws, int maxc, int cb, int m_rows,
                                                                       int p0, float* out, _Float16* out_hi,
                                                                       _Float16* out_lo, int ldo, int lo8) {
@@ -560,7 +863,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const floa
         for (int i = 0; i < 8; ++i) acc[i] = 0.f;
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
-            const float wgt = c < nch ? expf(mc[c] - M) : 0.f;  // 0 for a fully masked chunk (m = -inf)
+            const float wgt = c < nch ? (L2 ? exp2f(mc[c] - M) : expf(mc[c] - M)) : 0.f;  // 0 for a fully masked chunk (m = -inf)
             L += lc[c] * wgt;
             const float v[8] = {oc[c][0].x, oc[c][0].y, oc[c][0].z, oc[c][0].w,
                                 oc[c][1].x, oc[c][1].y, oc[c][1].z, oc[c][1].w};
@@ -609,6 +912,9 @@ int prefill_finish_launch(DecodeState* st, const int32_t* prompt, int32_t* token
     return LLMI_OK;
 }
 
+static std::atomic<unsigned long long*> g_pf_stamps{nullptr};
+void prefill_stamps_debug(unsigned long long* stamps) { g_pf_stamps.store(stamps); }
+
 int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
     LLMI_REQUIRE(a.qkv && a.k_cache && a.v_cache && a.rope_tab, "prefill attention: null argument");
     LLMI_REQUIRE(a.head_dim == D, "prefill attention: head_dim must be 128");
@@ -632,7 +938,14 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
                 max_nkb = std::max(max_nkb, pf_nkb(qb, a.p0, a.m));
             }
             // (189-214 VGPRs: two workgroups per CU, so ~512 workgroups run in one round)
-            int cb = a.split_ws ? std::max(2, (blocks * a.heads + 511) / 512) : max_nkb;
+            static const bool old_form = [] {  // A/B knob: LLMI_PF_ATTN=reg (the register-staged form)
+                const char* e = std::getenv("LLMI_PF_ATTN");
+                return e && std::string(e) == "reg";
+            }();
+            // the register-staged form splits keys into chunks of cb blocks (~512 workgroups, two
+            // per CU); the transposed form runs whole query blocks (one 8-wave workgroup per CU,
+            // deep copy pipeline: no partials to write and merge)
+            int cb = a.split_ws && old_form ? std::max(2, (blocks * a.heads + 511) / 512) : max_nkb;
             static const int cb_env = [] {  // tuning knob: key blocks per chunk (LLMI_PF_CHUNK)
                 const char* e = std::getenv("LLMI_PF_CHUNK");
                 return e ? std::atoi(e) : 0;
@@ -647,18 +960,29 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
             for (int qb = 0; qb < nqb; ++qb) grid += (pf_nkb(qb, a.p0, a.m) + cb - 1) / cb;
             // 1-D, XCD-interleaved: 8 x ceil(heads / 8) x (items per head) workgroups
             const dim3 gm(8 * ((a.heads + 7) / 8) * grid);
-            if (a.mfma_planes == 2)
-                hipLaunchKernelGGL(attn_prefill_mfma_kernel<2>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
-                                   a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
-                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc, a.out_lo8);
-            else
-                hipLaunchKernelGGL(attn_prefill_mfma_kernel<1>, gm, dim3(kThreads), 0, s, a.qkv, ld, a.m, a.p0,
-                                   a.heads, a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq,
-                                   a.out, a.out_hi, a.out_lo, a.heads * D, cb, a.split_ws, maxc, a.out_lo8);
+#define PF_ATTN(K, PL, NT, ...)                                                                               \
+    hipLaunchKernelGGL(K<PL>, gm, dim3(NT), 0, s, a.qkv, ld, a.m, a.p0, a.heads, a.kv_heads,                  \
+                       (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq, a.out, a.out_hi, a.out_lo, \
+                       a.heads * D, cb, a.split_ws, maxc, a.out_lo8 __VA_ARGS__)
+            if (old_form) {
+                if (a.mfma_planes == 2) PF_ATTN(attn_prefill_mfma_kernel, 2, kThreads);
+                else PF_ATTN(attn_prefill_mfma_kernel, 1, kThreads);
+            } else {
+                unsigned long long* st = g_pf_stamps.load(std::memory_order_relaxed);
+                if (a.mfma_planes == 2) PF_ATTN(attn_prefill_tr_kernel, 2, kTrThreads, , st);
+                else PF_ATTN(attn_prefill_tr_kernel, 1, kTrThreads, , st);
+            }
+#undef PF_ATTN
             if (maxc > 1) {
-#define PF_MERGE(C)                                                                                              \
-    hipLaunchKernelGGL(attn_prefill_merge_kernel<C>, dim3(nqb, a.heads), dim3(kThreads), 0, s, a.split_ws, maxc, cb, \
-                       a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D, a.out_lo8)
+#define PF_MERGE(C)                                                                                                 \
+    do {                                                                                                            \
+        if (old_form)                                                                                               \
+            hipLaunchKernelGGL((attn_prefill_merge_kernel<C, false>), dim3(nqb, a.heads), dim3(kThreads), 0, s,     \
+                               a.split_ws, maxc, cb, a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D, a.out_lo8); \
+        else                                                                                                        \
+            hipLaunchKernelGGL((attn_prefill_merge_kernel<C, true>), dim3(nqb, a.heads), dim3(kThreads), 0, s,      \
+                               a.split_ws, maxc, cb, a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D, a.out_lo8); \
+    } while (0)
                 if (maxc <= 2)
                     PF_MERGE(2);
                 else if (maxc <= 4)

@@ -68,6 +68,7 @@ _SIGS = {
     "llmi_ffn_residual": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P]),
     "llmi_stream_errors": (_I, [_P, _P]),
     "llmi_debug_stream_k": (_I, [_I, _I]),
+    "llmi_debug_prefill_stamps": (_I, [_P]),
     "llmi_hbm_read_bench": (_I, [_SZ, _I, _P, _P, _P]),
     "llmi_batched_matmul": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "llmi_transpose_remove_pad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
