@@ -20,7 +20,6 @@
 #include <atomic>
 
 #include <cstdlib>
-#include <string>
 
 #include "kernels.h"
 
@@ -217,31 +216,21 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_kernel(const float* qkv
     }
 }
 
-// ---- MFMA form for the fp16 cache (engine prefill). Workgroup = (64 query rows,
-// head): wave w owns rows 16 w .. 16 w + 15. Per 64-key block of the causal range:
-//   S = Q K^T     v_mfma_f32_16x16x32_f16, Q fragments in registers (q * 1/sqrt(d)
-//                 split into P fp16 planes), K staged in LDS [key][dim] with the
-//                 16-B chunk index XOR (key & 15): a B fragment's 16 rows hit 16
-//                 distinct bank groups;
-//   online softmax on the accumulator layout (rows 4 (lane >> 4) + r), fp32 expf;
-//   O += P V      P through a per-wave LDS image (C layout -> A layout, P planes),
-//                 V staged transposed [dim][key] (chunk XOR (dim & 7)).
-// The next block's K/V rows are loaded into registers before this block's MFMAs
-// (register double buffer). P = 2 (hi + lo planes of q and of p against the exact
-// fp16 K, V) is fp32-faithful; P = 1 is the fp16 throughput mode. Output: fp32 rows,
-// or the o_proj GEMM's fp16 input planes directly.
+// ---- MFMA form for the fp16 cache (engine prefill): attn_prefill_tr_kernel below. P = 2
+// (hi + lo fp16 planes of q and of p against the exact fp16 K, V) is fp32-faithful; P = 1
+// is the fp16 throughput mode. Output: fp32 rows, or the o_proj GEMM's fp16 input planes.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int QM = 64;  // query rows per workgroup
-__device__ __forceinline__ int vswz(int d) { return (d ^ (d >> 3)) & 7; }  // Vt row d's 16-B chunk XOR
 constexpr int KB = 64;  // keys per block
 
-// Split keys: the causal range of query block qb (key blocks [0, nkb(qb))) is cut into
-// chunks of cb key blocks, one workgroup each (~512: two fit per CU), so the longest query blocks no longer set
-// the kernel's critical path (8 dependent key blocks at M = 512). A query block with one
-// chunk writes its output directly; otherwise every chunk writes its unnormalised
-// (O, m, l) to ws[head][qb][chunk] and attn_prefill_merge_kernel combines them in
-// chunk order. blockIdx.x enumerates (qb, chunk), longest query blocks first.
+// Split keys: the causal range of query block qb (key blocks [0, nkb(qb))) can be cut into
+// chunks of cb key blocks, one workgroup each -- used when whole query blocks leave CUs
+// idle (few rows after a long history: one chunk of 64 rows at p0 = 1984 is 32 workgroups
+// of 32 dependent blocks). A query block with one chunk writes its output directly;
+// otherwise every chunk writes its unnormalised (O, m, l) to ws[head][qb][chunk] and
+// attn_prefill_merge_kernel combines them in chunk order. blockIdx.x enumerates
+// (qb, chunk), longest query blocks first.
 // workgroup size of rope_kv_prefill_kernel (LLMI_ROPE_THREADS, A/B; default 1024)
 inline int pf_rope_threads() {
     static const int v = [] {
@@ -257,276 +246,9 @@ __host__ __device__ inline int pf_nkb(int qb, int p0, int m_rows) {
 }
 constexpr int kPartFloats = QM * D + 2 * QM;  // one chunk's O rows, then m, then l
 
-template <int P>
-__global__ __launch_bounds__(kThreads) void attn_prefill_mfma_kernel(const float* qkv, int ld, int m_rows, int p0,
-                                                                     int heads, int kv_heads, const __half* k_cache,
-                                                                     const __half* v_cache, int max_seq, float* out,
-                                                                     _Float16* out_hi, _Float16* out_lo, int ldo,
-                                                                     int cb, float* ws, int maxc, int lo8) {
-    __shared__ __attribute__((aligned(16))) char smem[KB * D * 2 + D * KB * 2 + 4 * P * 16 * KB * 2];
-    char* Ks = smem;                 // [key][256 B], chunk ^= key & 15
-    char* Vt = smem + KB * D * 2;    // [dim][128 B], chunk ^= vswz(dim)
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int fr = lane & 15, fq = lane >> 4;
-    char* Pw = Vt + D * KB * 2 + w * P * 16 * KB * 2;  // this wave's [P][16][128 B], chunk ^= row & 7
-
-    const int nqb = (m_rows + QM - 1) / QM;
-    // XCD-aware 1-D grid (workgroup id % 8 = its XCD): every (query block, chunk) of one head
-    // runs on the same XCD, so that XCD's L2 holds the head's K / V for all of them (spread
-    // over the XCDs, each L2 saw every head's K / V, 8 MB at 7B width and 512 rows)
-    const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;
-    const int per = (heads - xcd + 7) / 8;  // heads xcd, xcd + 8, ... live on this XCD
-    int items = 0;  // (query block, chunk) items per head
-    for (int q = 0; q < nqb; ++q) items += (pf_nkb(q, p0, m_rows) + cb - 1) / cb;
-    if (r >= per * items) return;
-    const int h = xcd + 8 * (r % per);
-    int qb = nqb - 1, chunk = 0, nch = 1;
-    for (int idx = r / per; qb >= 0; --qb) {  // longest (latest) query blocks first
-        nch = (pf_nkb(qb, p0, m_rows) + cb - 1) / cb;
-        if (idx < nch) {
-            chunk = idx;
-            break;
-        }
-        idx -= nch;
-    }
-    const int kvh = h / (heads / kv_heads);
-    const int q_first = qb * QM;
-    const float qscale = 1.0f / sqrtf((float)D);
-
-    // Q fragments: row q_first + 16 w + fr, dims 32 ks + 8 fq + [0, 8). The raw loads go
-    // out first, then the first K/V block's (below), then the conversion: one round trip
-    h8 qa[P][4];
-    float4 qraw[4][2];
-    {
-        const int qrow = min(q_first + 16 * w + fr, m_rows - 1);
-        const float* qp = qkv + (size_t)qrow * ld + (size_t)h * D;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            qraw[ks][0] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq);
-            qraw[ks][1] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq + 4);
-        }
-    }
-
-    const int kend = p0 + min(q_first + QM, m_rows);  // keys [0, kend)
-    const int nkb = (kend + KB - 1) / KB;
-    const int kb0 = chunk * cb, kb1 = min(kb0 + cb, nkb);  // this workgroup's key blocks
-    const __half* kc = k_cache + (size_t)kvh * max_seq * D;
-    const __half* vc = v_cache + (size_t)kvh * max_seq * D;
-    // staging: thread t moves 16 B (8 dims) of key rows t / 16 + 16 i, chunk t % 16
-    const int sr = t >> 4, sc = t & 15;
-    uint4 kreg[4], vreg[4];
-    // K: key rows sr + 16 i (i < 4); V: key PAIRS 2 (sr + 16 i), +1 (i < 2), so each
-    // transposed store writes two keys of one dim (4 B) -- half the stores of a
-    // per-key transpose, and the Vt chunk swizzle (d ^ d >> 3) & 7 spreads them over the banks
-    auto gload = [&](int kb) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int key = min(kb * KB + sr + 16 * i, kend - 1);
-            kreg[i] = *reinterpret_cast<const uint4*>(kc + (size_t)key * D + sc * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int k0 = kb * KB + 2 * (sr + 16 * i);
-            vreg[2 * i] = *reinterpret_cast<const uint4*>(vc + (size_t)min(k0, kend - 1) * D + sc * 8);
-            vreg[2 * i + 1] = *reinterpret_cast<const uint4*>(vc + (size_t)min(k0 + 1, kend - 1) * D + sc * 8);
-        }
-    };
-    auto lstore = [&]() {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = sr + 16 * i;
-            *reinterpret_cast<uint4*>(Ks + r * 256 + ((sc ^ (r & 15)) << 4)) = kreg[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int r0 = 2 * (sr + 16 * i);
-            const _Float16* h0 = reinterpret_cast<const _Float16*>(&vreg[2 * i]);
-            const _Float16* h1 = reinterpret_cast<const _Float16*>(&vreg[2 * i + 1]);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int d = sc * 8 + e;
-                typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-                *reinterpret_cast<h2*>(Vt + d * 128 + (((r0 >> 3) ^ vswz(d)) << 4) + (r0 & 7) * 2) = h2{h0[e], h1[e]};
-            }
-        }
-    };
-
-    float m_run[4], l_run[4];
-    f4 o[8];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        m_run[r] = -INFINITY;
-        l_run[r] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f4{0.f, 0.f, 0.f, 0.f};
-    const int qpos0 = p0 + q_first + 16 * w + 4 * fq;  // position of accumulator row r: qpos0 + r
-
-    gload(kb0);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        const float v[8] = {qraw[ks][0].x, qraw[ks][0].y, qraw[ks][0].z, qraw[ks][0].w,
-                            qraw[ks][1].x, qraw[ks][1].y, qraw[ks][1].z, qraw[ks][1].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float x = v[e] * qscale;
-            const _Float16 hi = (_Float16)x;
-            qa[0][ks][e] = hi;
-            if (P == 2) qa[P - 1][ks][e] = (_Float16)(x - (float)hi);
-        }
-    }
-    for (int kb = kb0; kb < kb1; ++kb) {
-        __syncthreads();  // every wave finished reading the previous block
-        lstore();
-        __syncthreads();
-        if (kb + 1 < kb1) gload(kb + 1);
-
-        f4 s[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s[j] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = 16 * j + fr;
-                const h8 bk = *reinterpret_cast<const h8*>(Ks + key * 256 + (((4 * ks + fq) ^ (key & 15)) << 4));
-#pragma unroll
-                for (int p = 0; p < P; ++p) s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[p][ks], bk, s[j], 0, 0, 0);
-            }
-        }
-        // causal mask (build_causal_mask.cu:29: key <= query position), online softmax
-        float mx[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            mx[r] = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = kb * KB + 16 * j + fr;
-                if (key > qpos0 + r || key >= kend) s[j][r] = -INFINITY;
-                mx[r] = fmaxf(mx[r], s[j][r]);
-            }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], off));
-        }
-        float alpha[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            // a chunk that starts after a row's position masks all of its keys for that
-            // row: m stays -inf, p = 0 (chunk 0 holds key 0, visible to every row)
-            const float m_new = fmaxf(m_run[r], mx[r]);
-            const float m_use = m_new == -INFINITY ? 0.f : m_new;
-            alpha[r] = expf(m_run[r] - m_use);
-            m_run[r] = m_new;
-            float ps = 0.f;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float pv = expf(s[j][r] - m_use);
-                s[j][r] = pv;
-                ps += pv;
-            }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) ps += __shfl_xor(ps, off);
-            l_run[r] = l_run[r] * alpha[r] + ps;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
-        // P (C layout: row 4 fq + r, key 16 j + fr) -> this wave's LDS image
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 4 * fq + r, key = 16 * j + fr;
-                const int off = row * 128 + (((key >> 3) ^ (row & 7)) << 4) + (key & 7) * 2;
-                const _Float16 hi = (_Float16)s[j][r];
-                *reinterpret_cast<_Float16*>(Pw + off) = hi;
-                if (P == 2) *reinterpret_cast<_Float16*>(Pw + 16 * KB * 2 + off) = (_Float16)(s[j][r] - (float)hi);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        // O += P V: A = P rows fr, keys 32 kk + 8 fq; B = V^T rows (dims) 16 jt + fr
-#pragma unroll
-        for (int kk = 0; kk < KB / 32; ++kk) {
-            h8 pa[P];
-#pragma unroll
-            for (int p = 0; p < P; ++p)
-                pa[p] = *reinterpret_cast<const h8*>(Pw + p * 16 * KB * 2 + fr * 128 + (((4 * kk + fq) ^ (fr & 7)) << 4));
-#pragma unroll
-            for (int jt = 0; jt < 8; ++jt) {
-                const int d = 16 * jt + fr;
-                const h8 bv = *reinterpret_cast<const h8*>(Vt + d * 128 + (((4 * kk + fq) ^ vswz(d)) << 4));
-#pragma unroll
-                for (int p = 0; p < P; ++p) o[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pa[p], bv, o[jt], 0, 0, 0);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();  // P image is rewritten next block
-    }
-
-    // epilogue through LDS (K/V/P images are free now): the O rows -- unnormalised for a
-    // partial, divided by l for a direct output -- as a padded fp32 image [64][132], then
-    // 16-B stores, 32 lanes per row (scalar stores spanned 4 rows per instruction)
-    __syncthreads();
-    float* img = reinterpret_cast<float*>(smem);
-    constexpr int kIs = D + 4;  // row stride: rows 4 apart land 16 banks apart
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int lr = 16 * w + 4 * fq + r;
-        const float sc = nch > 1 ? 1.f : 1.0f / l_run[r];
-#pragma unroll
-        for (int jt = 0; jt < 8; ++jt) img[lr * kIs + 16 * jt + fr] = o[jt][r] * sc;
-    }
-    if (nch > 1) {  // partial: unnormalised O rows, m, l of this chunk
-        float* part = ws + ((size_t)(h * nqb + qb) * maxc + chunk) * kPartFloats;
-        if (fr == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int lr = 16 * w + 4 * fq + r;
-                part[QM * D + lr] = m_run[r];
-                part[QM * D + QM + lr] = l_run[r];
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < QM * D / 4 / kThreads; ++i) {
-            const int f = i * kThreads + t, lr = f >> 5, c4 = f & 31;
-            reinterpret_cast<float4*>(part)[f] = *reinterpret_cast<const float4*>(img + lr * kIs + 4 * c4);
-        }
-        return;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < QM * D / 8 / kThreads; ++i) {
-        const int f = i * kThreads + t, lr = f >> 4, c8 = f & 15;
-        const int row = q_first + lr;
-        if (row >= m_rows) continue;
-        const float4 x0 = *reinterpret_cast<const float4*>(img + lr * kIs + 8 * c8);
-        const float4 x1 = *reinterpret_cast<const float4*>(img + lr * kIs + 8 * c8 + 4);
-        const size_t idx = (size_t)row * ldo + (size_t)h * D + 8 * c8;
-        if (out_hi) {
-            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            h8 hv, lv;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                hv[e] = (_Float16)v[e];
-                lv[e] = (_Float16)(v[e] - (float)hv[e]);
-            }
-            *reinterpret_cast<h8*>(out_hi + idx) = hv;
-            if (out_lo && lo8)
-                *reinterpret_cast<uint2*>(reinterpret_cast<char*>(out_lo + (size_t)row * ldo) + (size_t)h * D + 8 * c8) =
-                    make_uint2(lo8_pack4(v[0] - (float)hv[0], v[1] - (float)hv[1], v[2] - (float)hv[2], v[3] - (float)hv[3]),
-                               lo8_pack4(v[4] - (float)hv[4], v[5] - (float)hv[5], v[6] - (float)hv[6], v[7] - (float)hv[7]));
-            else if (out_lo)
-                *reinterpret_cast<h8*>(out_lo + idx) = lv;
-        } else {
-            *reinterpret_cast<float4*>(out + idx) = x0;
-            *reinterpret_cast<float4*>(out + idx + 4) = x1;
-        }
-    }
-}
-
-// ---- Transposed form (round 5). Workgroup = (64 query rows, head, key chunk) as in
-// attn_prefill_mfma_kernel, but 8 waves: wave w owns query rows 16 (w & 3) .. + 15 and the
+// ---- Transposed form (round 5; it replaced a 4-wave register-staged kernel that put P
+// and a transposed V through LDS writes: 27.3 us + a 7.3-us merge launch per 7B layer at
+// M = 512, r05p). Workgroup = (64 query rows, head, key chunk), 8 waves: wave w owns query rows 16 (w & 3) .. + 15 and the
 // key HALF kp = w >> 2 (keys 32 kp .. 32 kp + 31) of every 64-key block, with its own online
 // softmax state; the two halves are combined once, in LDS, at the end. The two products are
 // oriented so that neither P nor V needs an LDS rewrite:
@@ -553,6 +275,25 @@ __device__ __forceinline__ int ksig(int g) { return ((g & 1) << 1) | (g >> 1); }
 __device__ __forceinline__ int vtr_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 __device__ __forceinline__ s4v tr_read(const char* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(p));
+}
+// butterfly reductions over lane ^ 16 / lane ^ 32 with the gfx950 row swaps (no LDS trip):
+// after v_permlane{16,32}_swap of x with itself the pair holds x[l] and x[l ^ 16 / 32], the
+// lower lane's value first, so every lane computes the same sum bit for bit
+__device__ __forceinline__ float xmax16(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xsum16(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 // global_load_lds_dwordx4 with a uniform base (SGPRs) and a per-lane 32-bit byte offset:
 // the wave's 64 lanes fill 1 KB of LDS from `lds` on, lane-linear
@@ -581,7 +322,9 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
     const int qt = w & 3, kp = w >> 2;  // query tile, key half
 
     const int nqb = (m_rows + QM - 1) / QM;
-    const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;  // XCD-aware order: attn_prefill_mfma_kernel
+    // XCD-aware 1-D grid (workgroup id % 8 = its XCD): every (query block, chunk) of one head
+    // runs on the same XCD, whose L2 then serves the head's K / V blocks to all of them
+    const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;
     const int per = (heads - xcd + 7) / 8;
     int items = 0;
     for (int q = 0; q < nqb; ++q) items += (pf_nkb(q, p0, m_rows) + cb - 1) / cb;
@@ -601,26 +344,20 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
     const float qscale = 1.4426950408889634f / sqrtf((float)D);  // log2(e) / sqrt(d)
 
     h8 qa[P][4];
-    float4 qraw[4][2];
-    {
-        const int qrow = min(q_first + 16 * qt + fr, m_rows - 1);
-        const float* qp = qkv + (size_t)qrow * ld + (size_t)h * D;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            qraw[ks][0] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq);
-            qraw[ks][1] = *reinterpret_cast<const float4*>(qp + 32 * ks + 8 * fq + 4);
-        }
-    }
     const int kend = p0 + min(q_first + QM, m_rows);
     const int nkb = (kend + KB - 1) / KB;
     const int kb0 = chunk * cb, kb1 = min(kb0 + cb, nkb);
     const void* kc = k_cache + (size_t)kvh * max_seq * D;
     const void* vc = v_cache + (size_t)kvh * max_seq * D;
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    // iteration i computes key block kb0 + i (a descending order measured the same, r05u)
+    const int nit = kb1 - kb0;
+    auto kb_of = [&](int i) { return kb0 + i; };
     // wave w fills 1-KB spans n = 8 i + w (image rows 4 n .. 4 n + 3) of both images: lane ->
     // row 4 n + lane / 16, physical chunk lane % 16 = logical chunk ^ swizzle. 4 copies per wave
-    auto issue = [&](int kb) {
-        const unsigned sb = lds0 + (unsigned)((kb - kb0) % kStages) * 2 * kImg;
+    auto issue = [&](int it) {
+        const int kb = kb_of(it);
+        const unsigned sb = lds0 + (unsigned)(it % kStages) * 2 * kImg;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int n = 8 * i + w, row = 4 * n + fq;
@@ -630,50 +367,35 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
             pf_glds(vc, src + ((fr ^ vtr_swz(row)) << 4), dst + kImg);
         }
     };
+    // the workgroup's 64 fp32 q rows (32 KB) go through the LDS of the last stage, which the
+    // first kStages - 1 blocks leave free: 512-B rows, 16-B chunk ch at ch ^ (row & 31), two
+    // rows per 1-KB span, 4 copies per wave. Every global read of the kernel is then a copy
+    // whose completion the kernel counts itself (a plain load's compiler-placed vmcnt wait
+    // would also wait for the K/V copies issued behind it)
+    char* qimg = smem + (kStages - 1) * 2 * kImg;
+    {
+        const unsigned qb0 = lds0 + (unsigned)(kStages - 1) * 2 * kImg;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = 8 * i + w, row = 2 * n + (lane >> 5), cp = lane & 31;
+            const unsigned src = (unsigned)min(q_first + row, m_rows - 1) * (unsigned)ld * 4u + (unsigned)h * D * 4u +
+                                 (unsigned)((cp ^ (row & 31)) << 4);
+            pf_glds(qkv, src, __builtin_amdgcn_readfirstlane(qb0 + n * 1024));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kStages - 1; ++i)
+        if (i < nit) issue(i);
 
     float m_run = -INFINITY, l_run = 0.f;  // this lane's query (column fr), log2 units
     f4 o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f4{0.f, 0.f, 0.f, 0.f};
     const int qpos = p0 + q_first + 16 * qt + fr;
-    const int qpos_max = p0 + q_first + 16 * qt + 15;               // the wave's last query
     const int arow = 32 * kp + 4 * ksig(fr >> 2) + (fr & 3);        // K image row of this A lane (tile 0)
-
-#pragma unroll
-    for (int i = 0; i < kStages - 1; ++i)
-        if (kb0 + i < kb1) issue(kb0 + i);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        const float v[8] = {qraw[ks][0].x, qraw[ks][0].y, qraw[ks][0].z, qraw[ks][0].w,
-                            qraw[ks][1].x, qraw[ks][1].y, qraw[ks][1].z, qraw[ks][1].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float x = v[e] * qscale;
-            const _Float16 hi = (_Float16)x;
-            qa[0][ks][e] = hi;
-            if (P == 2) qa[P - 1][ks][e] = (_Float16)(x - (float)hi);
-        }
-    }
-    if (ts.p && t == 0) {
-        ts.p[5] = (unsigned long long)qb | (unsigned long long)h << 16;
-        ts.p[6] = (unsigned long long)(kb1 - kb0);
-    }
-    const int tq = fr >> 2, tp = fr & 3;
-    for (int kb = kb0; kb < kb1; ++kb) {
-        // copies in flight behind block kb: min(kStages - 2, kb1 - 1 - kb) blocks of 4 per wave
-        const int ahead = min(kStages - 2, kb1 - 1 - kb);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // every wave's copies of block kb landed; stage of kb - 1 is free
-        if (kb == kb0) ts.mark(1);
-        if (kb + kStages - 1 < kb1) issue(kb + kStages - 1);
-        // a key half entirely past the wave's last query contributes nothing (wave-uniform)
-        if (kb * KB + 32 * kp > qpos_max) continue;
-        const char* Ks = smem + ((kb - kb0) % kStages) * 2 * kImg;
-        const char* Vs = Ks + kImg;
-
-        f4 s[2];
+    // S^T tile pair of iteration it: s[j][e] = score of key kb * KB + 32 kp + 16 j + 4 ksig(fq) + e
+    auto qk = [&](int it, f4 (&s)[2]) {
+        const char* Ks = smem + (it % kStages) * 2 * kImg;
         s[0] = s[1] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -685,10 +407,52 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
                 for (int p = 0; p < P; ++p) s[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ak, qa[p][ks], s[j], 0, 0, 0);
             }
         }
-        // s[j][e]: key kb * KB + 32 kp + 16 j + 4 ksig(fq) + e for query qpos. Causal mask
-        // (build_causal_mask.cu:29: key <= query position) only where the half reaches past
-        // the wave's first query or the keys' end (wave-uniform test)
-        const int kbase = kb * KB + 32 * kp;
+    };
+
+    // q and block 0 landed (blocks 1, 2 may still be in flight), for every wave
+    if (nit > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (nit > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ts.mark(1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const int row = 16 * qt + fr;
+        const float* qr = reinterpret_cast<const float*>(qimg + row * 512);
+        const float4 x0 = *reinterpret_cast<const float4*>(qr + 4 * ((8 * ks + 2 * fq) ^ (row & 31)));
+        const float4 x1 = *reinterpret_cast<const float4*>(qr + 4 * ((8 * ks + 2 * fq + 1) ^ (row & 31)));
+        const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float x = v[e] * qscale;
+            const _Float16 hi = (_Float16)x;
+            qa[0][ks][e] = hi;
+            if (P == 2) qa[P - 1][ks][e] = (_Float16)(x - (float)hi);
+        }
+    }
+    if (ts.p && t == 0) {
+        ts.p[5] = (unsigned long long)qb | (unsigned long long)h << 16;
+        ts.p[6] = (unsigned long long)nit;
+    }
+    __syncthreads();  // every wave read its q: the last stage is free for block kStages - 1
+    const int tq = fr >> 2, tp = fr & 3;
+    const int qpos_max = p0 + q_first + 16 * qt + 15;  // the wave's last query
+    for (int it = 0; it < nit; ++it) {
+        if (it > 0) {
+            // block it landed; blocks it + 1, it + 2 may still be in flight
+            const int ahead = min(kStages - 2, nit - 1 - it);
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // ... for every wave; and every wave is done with iteration it - 1
+        }
+        if (it + kStages - 1 < nit) issue(it + kStages - 1);  // into iteration it - 1's stage
+        const int kbase = kb_of(it) * KB + 32 * kp;
+        if (kbase > qpos_max) continue;  // the half has no key visible to the wave's queries
+        f4 s[2];
+        qk(it, s);
+        // causal mask (build_causal_mask.cu:29: key <= query position), only where the half
+        // reaches past the wave's first query or the keys' end (wave-uniform test)
         if (kbase + 31 > p0 + q_first + 16 * qt || kbase + 31 >= kend) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
@@ -698,15 +462,24 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
                     if (key > qpos || key >= kend) s[j][e] = -INFINITY;
                 }
         }
+        // Online softmax with a lazy reference: p = 2^(s - m_run) and m_run is raised (O, l
+        // rescaled) only when a score exceeds it by more than kTau = 8, so p <= 256 (exact in
+        // the fp16 planes' range) and the rescale -- a pass over the 32 accumulators -- is
+        // skipped by the whole wave on almost every block after the first
         float mx = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
                          fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        // a query with every key of the half masked: m stays -inf, p = 0
-        const float m_new = fmaxf(m_run, mx);
-        const float m_use = m_new == -INFINITY ? 0.f : m_new;
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
-        m_run = m_new;
+        mx = xmax16(mx);
+        mx = xmax32(mx);
+        constexpr float kTau = 8.f;
+        if (__builtin_amdgcn_ballot_w64(mx > m_run + kTau) != 0) {
+            const float m_new = mx > m_run + kTau ? mx : m_run;
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 0 from -inf, 1 if unchanged
+            m_run = m_new;
+            l_run *= alpha;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] *= alpha;
+        }
+        const float m_use = m_run == -INFINITY ? 0.f : m_run;  // every key so far masked: p = 0
         float ps = 0.f;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -716,11 +489,9 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
                 s[j][e] = pv;
                 ps += pv;
             }
-        ps += __shfl_xor(ps, 16);
-        ps += __shfl_xor(ps, 32);
-        l_run = l_run * alpha + ps;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] *= alpha;
+        ps = xsum16(ps);
+        ps = xsum32(ps);
+        l_run += ps;
 
         // O^T += V^T P^T over the half's 32 keys: P^T element e = s[e / 4][e % 4]; the V^T
         // fragment's elements 0-3 / 4-7 are the transposed reads of image rows
@@ -733,6 +504,7 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
             pb[0][e] = hi;
             if (P == 2) pb[P - 1][e] = (_Float16)(x - (float)hi);
         }
+        const char* Vs = smem + (it % kStages) * 2 * kImg + kImg;
         const int row0 = 32 * kp + 4 * ksig(fq) + tq;  // row0 + 16 has the same swizzle
         const char* vrow0 = Vs + row0 * 256 + 8 * (tp & 1);
 #pragma unroll
@@ -749,7 +521,7 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
     // epilogue. o[dt][e] = O[query 16 qt + fr][dim 16 dt + 4 fq + e] of this key half.
     // Half 1 leaves (O, m, l) in LDS; half 0 combines: M = max, a_i = 2^(m_i - M),
     // L = l_0 a_0 + l_1 a_1, O = O_0 a_0 + O_1 a_1 (/ L for a direct output), into the padded
-    // fp32 image that the 16-B store loop of attn_prefill_mfma_kernel reads.
+    // fp32 image that the 16-B row stores below read (32 lanes per row).
     constexpr int kIs = D + 4;
     __syncthreads();  // every wave is done with the stages (no copy is in flight)
     ts.mark(2);
@@ -831,7 +603,7 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
 // of 16 rows; thread t: row 16 pass + t / 16, dims 8 (t % 16) .. + 8, so 16 lanes cover a
 // row with 16-B loads and stores. Every chunk's loads are issued before any is used
 // (MAXC slots, clamped chunk index, unused slots weighted 0): one memory round trip.
-template <int MAXC, bool L2>  // L2: the partials' m are in log2 units (attn_prefill_tr_kernel)
+template <int MAXC>  // the partials' m are in log2 units (attn_prefill_tr_kernel)
 __global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const float* ws, int maxc, int cb, int m_rows,
                                                                       int p0, float* out, _Float16* out_hi,
                                                                       _Float16* out_lo, int ldo, int lo8) {
@@ -863,7 +635,7 @@ __global__ __launch_bounds__(kThreads) void attn_prefill_merge_kernel(const floa
         for (int i = 0; i < 8; ++i) acc[i] = 0.f;
 #pragma unroll
         for (int c = 0; c < MAXC; ++c) {
-            const float wgt = c < nch ? (L2 ? exp2f(mc[c] - M) : expf(mc[c] - M)) : 0.f;  // 0 for a fully masked chunk (m = -inf)
+            const float wgt = c < nch ? exp2f(mc[c] - M) : 0.f;  // 0 for a fully masked chunk (m = -inf)
             L += lc[c] * wgt;
             const float v[8] = {oc[c][0].x, oc[c][0].y, oc[c][0].z, oc[c][0].w,
                                 oc[c][1].x, oc[c][1].y, oc[c][1].z, oc[c][1].w};
@@ -937,15 +709,16 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
                 blocks += pf_nkb(qb, a.p0, a.m);
                 max_nkb = std::max(max_nkb, pf_nkb(qb, a.p0, a.m));
             }
-            // (189-214 VGPRs: two workgroups per CU, so ~512 workgroups run in one round)
-            static const bool old_form = [] {  // A/B knob: LLMI_PF_ATTN=reg (the register-staged form)
-                const char* e = std::getenv("LLMI_PF_ATTN");
-                return e && std::string(e) == "reg";
+            // one 8-wave workgroup per CU (128 KB of LDS): whole query blocks when they give
+            // every CU one; otherwise chunks of cb key blocks sized for ~one workgroup per CU
+            static const int n_cu = [] {
+                int dev = 0, n = 256;
+                if (hipGetDevice(&dev) == hipSuccess)
+                    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+                return n > 0 ? n : 256;
             }();
-            // the register-staged form splits keys into chunks of cb blocks (~512 workgroups, two
-            // per CU); the transposed form runs whole query blocks (one 8-wave workgroup per CU,
-            // deep copy pipeline: no partials to write and merge)
-            int cb = a.split_ws && old_form ? std::max(2, (blocks * a.heads + 511) / 512) : max_nkb;
+            int cb = max_nkb;
+            if (a.split_ws && nqb * a.heads < n_cu) cb = std::max(1, (blocks * a.heads + n_cu - 1) / n_cu);
             static const int cb_env = [] {  // tuning knob: key blocks per chunk (LLMI_PF_CHUNK)
                 const char* e = std::getenv("LLMI_PF_CHUNK");
                 return e ? std::atoi(e) : 0;
@@ -956,33 +729,25 @@ int prefill_attn_launch(const PrefillAttnArgs& a, hipStream_t s) {
                 cb = max_nkb;  // no room: one chunk per query block
                 maxc = 1;
             }
+            if (!a.split_ws) cb = max_nkb, maxc = 1;
             int grid = 0;
             for (int qb = 0; qb < nqb; ++qb) grid += (pf_nkb(qb, a.p0, a.m) + cb - 1) / cb;
             // 1-D, XCD-interleaved: 8 x ceil(heads / 8) x (items per head) workgroups
             const dim3 gm(8 * ((a.heads + 7) / 8) * grid);
-#define PF_ATTN(K, PL, NT, ...)                                                                               \
-    hipLaunchKernelGGL(K<PL>, gm, dim3(NT), 0, s, a.qkv, ld, a.m, a.p0, a.heads, a.kv_heads,                  \
-                       (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq, a.out, a.out_hi, a.out_lo, \
-                       a.heads * D, cb, a.split_ws, maxc, a.out_lo8 __VA_ARGS__)
-            if (old_form) {
-                if (a.mfma_planes == 2) PF_ATTN(attn_prefill_mfma_kernel, 2, kThreads);
-                else PF_ATTN(attn_prefill_mfma_kernel, 1, kThreads);
-            } else {
-                unsigned long long* st = g_pf_stamps.load(std::memory_order_relaxed);
-                if (a.mfma_planes == 2) PF_ATTN(attn_prefill_tr_kernel, 2, kTrThreads, , st);
-                else PF_ATTN(attn_prefill_tr_kernel, 1, kTrThreads, , st);
-            }
+            unsigned long long* st = g_pf_stamps.load(std::memory_order_relaxed);
+#define PF_ATTN(PL)                                                                                            \
+    hipLaunchKernelGGL(attn_prefill_tr_kernel<PL>, gm, dim3(kTrThreads), 0, s, a.qkv, ld, a.m, a.p0, a.heads,  \
+                       a.kv_heads, (const __half*)a.k_cache, (const __half*)a.v_cache, a.max_seq, a.out, a.out_hi, \
+                       a.out_lo, a.heads * D, cb, a.split_ws, maxc, a.out_lo8, st)
+            if (a.mfma_planes == 2)
+                PF_ATTN(2);
+            else
+                PF_ATTN(1);
 #undef PF_ATTN
             if (maxc > 1) {
-#define PF_MERGE(C)                                                                                                 \
-    do {                                                                                                            \
-        if (old_form)                                                                                               \
-            hipLaunchKernelGGL((attn_prefill_merge_kernel<C, false>), dim3(nqb, a.heads), dim3(kThreads), 0, s,     \
-                               a.split_ws, maxc, cb, a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D, a.out_lo8); \
-        else                                                                                                        \
-            hipLaunchKernelGGL((attn_prefill_merge_kernel<C, true>), dim3(nqb, a.heads), dim3(kThreads), 0, s,      \
-                               a.split_ws, maxc, cb, a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D, a.out_lo8); \
-    } while (0)
+#define PF_MERGE(C)                                                                                              \
+    hipLaunchKernelGGL(attn_prefill_merge_kernel<C>, dim3(nqb, a.heads), dim3(kThreads), 0, s, a.split_ws, maxc, cb, \
+                       a.m, a.p0, a.out, a.out_hi, a.out_lo, a.heads * D, a.out_lo8)
                 if (maxc <= 2)
                     PF_MERGE(2);
                 else if (maxc <= 4)
