@@ -259,9 +259,9 @@ constexpr int kPartFloats = QM * D + 2 * QM;  // one chunk's O rows, then m, the
 //                 wave's half, converted to fp16 planes in registers), A = V^T read from a
 //                 ROW-major V image with ds_read_b64_tr_b16 (the hardware transpose).
 // K and V are copied HBM -> LDS by global_load_lds_dwordx4 (no register staging) through a
-// ring of kStages 32-KB stages, kStages - 1 blocks in flight ahead of the one computed:
-// the kernel was DMA-latency-bound with one block of look-ahead (r05p: 22.2 us / layer
-// without key chunks, 2.7 us per block on the critical path). The swizzles are applied by
+// ring of kStages = 4 32-KB stages worked in pairs: the pair being computed and the next pair
+// in flight, one barrier per pair (r05p: 22.2 us / layer with a single block of look-ahead;
+// the copies never gate the loop now, r05t). The swizzles are applied by
 // permuting each lane's SOURCE chunk (the DMA writes lane-linear 1 KB spans).
 // Key order inside a 16-key tile: the A-operand lane of row i reads key kperm(i) =
 // 4 ksig(i >> 2) + (i & 3) (ksig = 0 2 1 3), so accumulator group fq holds keys
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
         }
     };
     // the workgroup's 64 fp32 q rows (32 KB) go through the LDS of the last stage, which the
-    // first kStages - 1 blocks leave free: 512-B rows, 16-B chunk ch at ch ^ (row & 31), two
+    // first pair of blocks leaves free: 512-B rows, 16-B chunk ch at ch ^ (row & 31), two
     // rows per 1-KB span, 4 copies per wave. Every global read of the kernel is then a copy
     // whose completion the kernel counts itself (a plain load's compiler-placed vmcnt wait
     // would also wait for the K/V copies issued behind it)
@@ -383,8 +383,7 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
             pf_glds(qkv, src, __builtin_amdgcn_readfirstlane(qb0 + n * 1024));
         }
     }
-#pragma unroll
-    for (int i = 0; i < kStages - 1; ++i)
+    for (int i = 0; i < 2; ++i)
         if (i < nit) issue(i);
 
     float m_run = -INFINITY, l_run = 0.f;  // this lane's query (column fr), log2 units
@@ -409,10 +408,8 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
         }
     };
 
-    // q and block 0 landed (blocks 1, 2 may still be in flight), for every wave
-    if (nit > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (nit > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // q and blocks 0, 1 landed, for every wave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     ts.mark(1);
 #pragma unroll
@@ -434,19 +431,21 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
         ts.p[5] = (unsigned long long)qb | (unsigned long long)h << 16;
         ts.p[6] = (unsigned long long)nit;
     }
-    __syncthreads();  // every wave read its q: the last stage is free for block kStages - 1
+    __syncthreads();  // every wave read its q: the last stage is free for block 3
     const int tq = fr >> 2, tp = fr & 3;
     const int qpos_max = p0 + q_first + 16 * qt + 15;  // the wave's last query
     for (int it = 0; it < nit; ++it) {
-        if (it > 0) {
-            // block it landed; blocks it + 1, it + 2 may still be in flight
-            const int ahead = min(kStages - 2, nit - 1 - it);
-            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // ... for every wave; and every wave is done with iteration it - 1
+        // two key blocks per barrier (r05ai: −0.4 µs a layer against one): at an even
+        // iteration blocks it, it + 1 have landed (issued one pair earlier) and every wave is
+        // done with it - 2, it - 1, whose stages take the next pair
+        if ((it & 1) == 0) {
+            if (it > 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+            if (it + 2 < nit) issue(it + 2);
+            if (it + 3 < nit) issue(it + 3);
         }
-        if (it + kStages - 1 < nit) issue(it + kStages - 1);  // into iteration it - 1's stage
         const int kbase = kb_of(it) * KB + 32 * kp;
         if (kbase > qpos_max) continue;  // the half has no key visible to the wave's queries
         f4 s[2];
