@@ -43,7 +43,7 @@ template <typename KT, bool HOST_SIZED>
 __global__ __launch_bounds__(kThreads) void attn_decode_kernel(AttnArgs a, int ns) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     WgStamp ts(a.stamps);
-    attn_body<KT, PlainIO, HOST_SIZED>(a, blockIdx.x, blockIdx.y, ns, smem);
+    attn_body<KT, PlainIO, HOST_SIZED>(a, blockIdx.x, blockIdx.y, ns, smem, &ts);
 }
 
 // Log-sum-exp merge of the split-KV partials of each head (one workgroup per

@@ -156,7 +156,8 @@ constexpr size_t kAttnLds = (3 * D + CH + (kThreads / LPR) * D + 4) * sizeof(flo
 // scalar load from memory another kernel just wrote) has arrived; rows past the
 // position are loaded (valid cache memory below max_seq) and ignored.
 template <typename KT, typename IO, bool HOST_SIZED = false>
-__device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, int ns, float* smem) {
+__device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, int ns, float* smem,
+                                          const WgStamp* ts = nullptr) {
     float* q_s = smem;
     float* kcur_s = q_s + D;
     float* vcur_s = kcur_s + D;
@@ -267,6 +268,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
         vcur_s[tid - D] = cache_round<KT>(HOST_SIZED ? pv : IO::ld(vrow + tid - D));
     }
     __syncthreads();
+    if (ts) ts->mark(1);  // timeline: q rotated, this split's K/V rows in registers
 
     if (owns_pos && (h % group) == 0 && tid < D) {
         // KV-cache write at slot pos (concat: fused_decoder_self_attention.cu:187-193,292-295)
@@ -294,8 +296,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
         float d = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) d = fmaf(qv[i], kv[i], d);
-#pragma unroll
-        for (int off = LPR / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, kWave);
+        d = row16_sum(d);  // LPR = 16: the group's lanes are one DPP row
         if (l16 == 0 && j < end) p_s[j - start] = d;
     }
     __syncthreads();
@@ -344,6 +345,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
         if (tid < D) a.out[(size_t)h * D + tid] = o / ml_s[1];
         return;
     }
+    if (ts) ts->mark(2);  // timeline: scores, softmax and P V done
     Ws ws = ws_carve(a.workspace, a.heads, ns);
     if (tid < D) IO::st(ws.o + ((size_t)h * ns + split) * D + tid, o);
     if (tid == 0) {
@@ -499,8 +501,7 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
             float acc = 0.f;
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc = fmaf((float)(int8_t)((q[i / 4] >> (8 * (i % 4))) & 0xff), x16[i], acc);
-#pragma unroll
-            for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+            acc = oct8_sum(acc);
             if ((l16 & 7) == 0) y_s[grp + 16 * (2 * u + (l16 >> 3))] = acc;
         }
     } else {
@@ -514,8 +515,7 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
         float acc = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc = fmaf(wv[i], xv[i], acc);
-#pragma unroll
-        for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+        acc = row16_sum(acc);
         if (l16 == 0) y_s[grp + 16 * t] = acc;
     }
     }

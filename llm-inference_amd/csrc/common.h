@@ -60,15 +60,64 @@ __device__ __forceinline__ float to_f32(float v) { return v; }
 __device__ __forceinline__ float to_f32(__half v) { return __half2float(v); }
 __device__ __forceinline__ float to_f32(int8_t v) { return (float)v; }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+// Cross-lane butterflies without the LDS crossbar (__shfl_xor compiles to ds_bpermute_b32:
+// an LDS round trip per step, on the critical path of every reduction tail). Lane ^ 32 and
+// ^ 16 use the gfx950 row swaps (v_permlane32_swap / v_permlane16_swap of x with itself: the
+// pair holds x[l] and x[l ^ 32 / 16]); lane ^ 8 ... ^ 1 use DPP row rotations, which equal the
+// xor partner once the earlier steps made the values symmetric (rotating a 16-lane row by 8
+// is ^ 8; after it, by 4 lands on a lane equal to l ^ 4, and so on). Each step adds the same
+// two values as the xor butterfly (a + b == b + a), so every sum and max keeps its exact bits.
+template <int N>
+__device__ __forceinline__ float row_ror(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + N, 0xF, 0xF,
+                                                                 false));
+}
+__device__ __forceinline__ float swap32_add(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap16_add(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap32_max(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float swap16_max(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// sum over each aligned 8-lane group (the xor 4, 2, 1 butterfly's association): lane ^ 4 is
+// the row shift left or right by 4, chosen by the lane's bit 2; ^ 2 and ^ 1 are quad permutes
+__device__ __forceinline__ float oct8_sum(float v) {
+    const float up = dpp<0x104>(v), down = dpp<0x114>(v);  // row_shl:4 / row_shr:4
+    v += (threadIdx.x & 4) ? down : up;
+    v += dpp<0x4E>(v);  // quad_perm [2, 3, 0, 1]
+    v += dpp<0xB1>(v);  // quad_perm [1, 0, 3, 2]
     return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+// sum over each aligned 16-lane group (the xor 8, 4, 2, 1 butterfly's association)
+__device__ __forceinline__ float row16_sum(float v) {
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    v += row_ror<2>(v);
+    v += row_ror<1>(v);
     return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {  // the xor 32, 16, ..., 1 butterfly
+    return row16_sum(swap16_add(swap32_add(v)));
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = swap16_max(swap32_max(v));
+    v = fmaxf(v, row_ror<8>(v));
+    v = fmaxf(v, row_ror<4>(v));
+    v = fmaxf(v, row_ror<2>(v));
+    return fmaxf(v, row_ror<1>(v));
 }
 
 // Block-wide sum for blockDim.x <= 1024; `red` needs >= 16 floats of LDS.

@@ -30,7 +30,7 @@ def wg_detail(host, stride, layer):
     round-robin dispatch) and the hardware CU id, for layer `layer`'s q/k/v, o and down, plus
     per-XCD completion quantiles: where a launch's tail comes from."""
     out = {}
-    for k, off in (("qkv", 0), ("o", 2), ("down", 4)):
+    for k, off in (("qkv", 0), ("attn", 1), ("o", 2), ("down", 4)):
         s = 5 * layer + off
         rows = host[s * stride:(s + 1) * stride].astype(np.int64)
         idx = np.nonzero(rows[:, 0] > 0)[0]
@@ -46,6 +46,11 @@ def wg_detail(host, stride, layer):
         out[k] = {"n": int(len(idx)), "end_quantiles_us": [round(float(q), 2) for q in
                                                             np.quantile(end, [0, 0.1, 0.5, 0.9, 0.99, 1.0])],
                   "start_max_us": round(float(start.max()), 2),
+                  # kernel-defined marks (attention: [1] q rotated + K/V rows in registers,
+                  # [2] P V done), quantiles [min, p50, max] in us from the launch's first start
+                  "mark_quantiles_us": {str(m): [round(float(q), 2) for q in np.quantile((v[v[:, m] > 0, m] - t0) / 100.0,
+                                                                                       [0, 0.5, 1.0])]
+                                        for m in (1, 2) if (v[:, m] > 0).any()},
                   "end_quantiles_by_xcd_us [min, p50, p90, max]": per_xcd,
                   "wg": [[int(i), round(float(a), 2), round(float(b), 2), int(r[4])]
                          for i, a, b, r in zip(idx, start, end, v)]}
