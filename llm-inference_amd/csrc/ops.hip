@@ -103,13 +103,39 @@ __global__ void rope_decode_kernel(float* qkv, int pos, int heads, int kv_heads,
 }
 
 // ------------------------------------------------- greedy argmax (two phase)
+// wave max of 64-bit keys with the row swaps and DPP row rotations of common.h's wave_max
+// (the max is exact whatever the pairing); both halves of a key move with the same permute
+__device__ __forceinline__ unsigned long long key_of(unsigned hi, unsigned lo) {
+    return (unsigned long long)hi << 32 | lo;
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned long long key_dpp(unsigned long long k) {
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(k >> 32), CTRL, 0xF, 0xF, false);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)k, CTRL, 0xF, 0xF, false);
+    const unsigned long long o = key_of(hi, lo);
+    return o > k ? o : k;
+}
+__device__ __forceinline__ unsigned long long wave_max_key(unsigned long long k) {
+    {
+        const auto h = __builtin_amdgcn_permlane32_swap((unsigned)(k >> 32), (unsigned)(k >> 32), false, false);
+        const auto l = __builtin_amdgcn_permlane32_swap((unsigned)k, (unsigned)k, false, false);
+        const unsigned long long a = key_of(h[0], l[0]), b = key_of(h[1], l[1]);
+        k = a > b ? a : b;
+    }
+    {
+        const auto h = __builtin_amdgcn_permlane16_swap((unsigned)(k >> 32), (unsigned)(k >> 32), false, false);
+        const auto l = __builtin_amdgcn_permlane16_swap((unsigned)k, (unsigned)k, false, false);
+        const unsigned long long a = key_of(h[0], l[0]), b = key_of(h[1], l[1]);
+        k = a > b ? a : b;
+    }
+    k = key_dpp<0x128>(k);  // row_ror:8
+    k = key_dpp<0x124>(k);  // row_ror:4
+    k = key_dpp<0x122>(k);  // row_ror:2
+    return key_dpp<0x121>(k);  // row_ror:1
+}
 __device__ unsigned long long block_max_key(unsigned long long k, unsigned long long* sh) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        unsigned long long o = __shfl_xor(k, off, kWave);
-        k = o > k ? o : k;
-    }
+    k = wave_max_key(k);
     __syncthreads();
     if (lane == 0) sh[w] = k;
     __syncthreads();
