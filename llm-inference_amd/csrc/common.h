@@ -101,6 +101,22 @@ __device__ __forceinline__ float oct8_sum(float v) {
     v += dpp<0xB1>(v);  // quad_perm [1, 0, 3, 2]
     return v;
 }
+// lane ^ 4 within aligned 8-lane groups: the row shift left or right by 4 by the lane's bit 2
+__device__ __forceinline__ float xor4(float v) {
+    const float up = dpp<0x104>(v), down = dpp<0x114>(v);  // row_shl:4 / row_shr:4
+    return (threadIdx.x & 4) ? down : up;
+}
+// the xor 1, 2, 4 butterfly over aligned 8-lane groups (quad permutes, then xor4)
+__device__ __forceinline__ float oct8_sum_up(float v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    return v + xor4(v);
+}
+__device__ __forceinline__ float oct8_max_up(float v) {
+    v = fmaxf(v, dpp<0xB1>(v));
+    v = fmaxf(v, dpp<0x4E>(v));
+    return fmaxf(v, xor4(v));
+}
 // sum over each aligned 16-lane group (the xor 8, 4, 2, 1 butterfly's association)
 __device__ __forceinline__ float row16_sum(float v) {
     v += row_ror<8>(v);

@@ -43,11 +43,7 @@ __global__ void causal_mask_kernel(T* mask, const int* q_lens, const int* k_lens
 }
 
 __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float o = __shfl_xor(v, off, kWave);
-        v = is_max ? fmaxf(v, o) : v + o;
-    }
+    v = is_max ? wave_max(v) : wave_sum(v);  // the xor 32 ... 1 butterfly (common.h)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     __syncthreads();
     if (lane == 0) sh[w] = v;
@@ -423,9 +419,7 @@ __global__ __launch_bounds__(kCThreads) void ctx_attn_kernel(const float* q, con
             sc[c] = (j > my_pos || j >= kend) ? -INFINITY : scale * sc[c];  // the reference's scale * qk
             mx = fmaxf(mx, sc[c]);
         }
-        mx = fmaxf(mx, __shfl_xor(mx, 1));
-        mx = fmaxf(mx, __shfl_xor(mx, 2));
-        mx = fmaxf(mx, __shfl_xor(mx, 4));
+        mx = oct8_max_up(mx);  // xor 1, 2, 4 (common.h)
         const float m_new = fmaxf(m_run, mx);  // finite: key 0 is always visible
         const float alpha = expf(m_run - m_new);
         float ps = 0.f;
@@ -435,9 +429,7 @@ __global__ __launch_bounds__(kCThreads) void ctx_attn_kernel(const float* q, con
             ps += pv;
             p_s[qi * (kCKC + 1) + kg + 8 * c] = pv;
         }
-        ps += __shfl_xor(ps, 1);
-        ps += __shfl_xor(ps, 2);
-        ps += __shfl_xor(ps, 4);
+        ps = oct8_sum_up(ps);
         l_run = l_run * alpha + ps;
         m_run = m_new;
         __builtin_amdgcn_wave_barrier();  // a p_s row is written and read by the same 8 lanes
@@ -618,8 +610,7 @@ __global__ __launch_bounds__(256, 2) void ctx_attn_mfma_kernel(const float* q, c
             p[1][qq] = (j1 > my_pos || j1 >= kend) ? -INFINITY : scale * s1[qq];
             mx = fmaxf(mx, fmaxf(p[0][qq], p[1][qq]));
         }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mx = swap32_max(swap16_max(mx));  // xor 16, then 32 (common.h)
         // a chunk wholly past this query's position leaves m at -inf and p = 0 (the wave's
         // first chunk may be such a chunk: only wave 0 starts at key 0)
         const float m_new = fmaxf(m_run, mx);
@@ -633,8 +624,7 @@ __global__ __launch_bounds__(256, 2) void ctx_attn_mfma_kernel(const float* q, c
                 p[tt][qq] = expf(p[tt][qq] - m_use);
                 ps += p[tt][qq];
             }
-        ps += __shfl_xor(ps, 16);
-        ps += __shfl_xor(ps, 32);
+        ps = swap32_add(swap16_add(ps));
         l_run = l_run * alpha + ps;
         m_run = m_new;
 #pragma unroll
