@@ -98,7 +98,11 @@ int llmi_linear(const float* x, const void* w, int w_dtype, const void* w_scales
  * trans_b = 1, trans_a = 0 is llmi_linear itself; the other forms transpose the operand(s)
  * into a per-(device, stream) scratch (grown outside stream capture: run the shape once
  * before capturing) and then run llmi_linear, so every form has llmi_linear's arithmetic.
- * f16 / f32 weights; int8 weights only with trans_b = 1 (their scales are per output row). */
+ * f16 / f32 weights; int8 weights only with trans_b = 1 (their scales are per output row).
+ * Cost: trans_b = 0 transposes the WHOLE weight on every call (one extra n*k read and write,
+ * so a weight-bound call moves ~3x the bytes of trans_b = 1); store weights [out, in] and pass
+ * trans_b = 1 on a hot path, as every reference layer does. The scratch is kept per (device,
+ * stream) for the process's lifetime, sized by the largest call. */
 int llmi_linear_trans(const float* x, const void* w, int w_dtype, const void* w_scales, float* y, int m, int n, int k,
                       int trans_a, int trans_b, llmi_stream_t stream);
 
@@ -132,7 +136,11 @@ int llmi_ffn_residual(const float* x, const void* w_gate_up, const void* w_down,
  * error word of their own -- llmi_linear / llmi_ffn / the *_residual calls: 16 = a stream-K
  * partial never arrived within 2 s (its workgroup could not run alongside the others), so
  * that output is incomplete. Synchronises the stream, stores the bits in *flags and clears
- * them. No counterpart in the reference (its cuBLAS calls have no cross-workgroup wait). */
+ * them. No counterpart in the reference (its cuBLAS calls have no cross-workgroup wait).
+ * Concurrency: the stream-K control words (epoch, arrival count) live in a per-(device,
+ * stream) workspace; launches on one workspace must not overlap, i.e. do not replay a graph
+ * captured on stream S on another stream while eager stream-K launches run on S (the epoch
+ * count would race silently). Launches on different streams use different workspaces. */
 int llmi_stream_errors(llmi_stream_t stream, int* flags);
 
 /* Test hook for the stream-K hand-off (no reference counterpart): the next `launches`

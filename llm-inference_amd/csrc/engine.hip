@@ -621,9 +621,14 @@ struct Engine {
     // its sums stay bitwise those of the fixtures' runs)
     int kpar_of(int groups) const {
         if (c.tp_world == 1 || kpar_off) return 0;
+        // the K-parted kernel stages x for k <= 5120 and splits a row's 16-B chunks evenly
+        // (a wider model must fall back to kpar 0, not fail the launch)
+        const int epl = wdt == LLMI_I8 ? 16 : wdt == LLMI_F16 ? 8 : 4;
+        if (c.hidden > 5120 || c.hidden % epl != 0) return 0;
         const int cus = n_cu > 0 ? n_cu : 256;
         const int blocks = (groups + 3) / 4;
-        return blocks < cus ? 4 : blocks < 2 * cus ? 2 : 0;
+        const int kp = blocks < cus ? 4 : blocks < 2 * cus ? 2 : 0;
+        return kp > 0 && (c.hidden / epl) % kp == 0 ? kp : 0;
     }
     bool kpar_off = false;
 

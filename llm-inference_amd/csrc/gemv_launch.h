@@ -112,8 +112,11 @@ int pick_unroll(const GemvArgs& a, int groups) {
     const int kl = (EPI == EPI_ATOMIC) ? a.k / a.ksplit : a.k;
     const int nc = kl / WT_<WT>::EPL / (a.kpar > 1 ? a.kpar : 1);  // chunks one wave streams
     auto slots = [&](int u) { const int b = kWave * u; return (nc + b - 1) / b * b; };
+    // kpar: only U = 4 is instantiated for the K-parted kernel (launch_u), so it is taken
+    // whatever the slot count (13B fp16 at kpar 2: 320 chunks a part would pick U = 5 and
+    // fail the launch)
+    if (a.kpar > 1) return 4;
     int best = (EPI != EPI_ARGMAX && groups >= 4096 && groups <= 12288 && kUnrollMax >= 4) ? 4 : kUnrollMax;
-    if (a.kpar > 1) best = 4;  // a K part is <= 2 batches of 4: fewest masked slots of {4, 5, 8}
     for (int u : {4, 5, 8})
         if (u <= kUnrollMax && slots(u) < slots(best)) best = u;
     return best;

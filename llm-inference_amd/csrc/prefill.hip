@@ -472,7 +472,10 @@ __global__ __launch_bounds__(kTrThreads) void attn_prefill_tr_kernel(const float
         constexpr float kTau = 8.f;
         if (__builtin_amdgcn_ballot_w64(mx > m_run + kTau) != 0) {
             const float m_new = mx > m_run + kTau ? mx : m_run;
-            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 0 from -inf, 1 if unchanged
+            // 0 from -inf, 1 if unchanged -- including a lane whose query still has every key
+            // masked (m_run = m_new = -inf) while another query of the wave fired the ballot:
+            // exp2(-inf - -inf) would be NaN there
+            const float alpha = m_new == m_run ? 1.f : __builtin_amdgcn_exp2f(m_run - m_new);
             m_run = m_new;
             l_run *= alpha;
 #pragma unroll

@@ -102,6 +102,20 @@ __device__ __forceinline__ void reduce_slice(const XchgArgs& a, int g, unsigned 
                 __builtin_amdgcn_s_sleep(2);
             }
         }
+        // The ordering this relies on, stated rather than implied: (1) the
+        // inboxes are hipDeviceMallocUncached (MTYPE UC), so payload and flag accesses bypass
+        // L1 / L2 on the producing and the consuming GPU alike, and each payload store is
+        // acknowledged (vmcnt 0, push_slice) before the flag store is issued; (2) every slot
+        // load below is a system-scope (sc0 sc1) load, issued after this poll. That is the
+        // write-through form of cdna_hip_programming.md Guideline 16 (every handed-off byte
+        // stored sc1 and drained, every load of it sc1), where the acquire reduces to an
+        // ordering point for the compiler -- which this fence is: it keeps the slot loads
+        // below the observation of the flag. A release / acquire pair at system scope would
+        // cost a whole-L2 write-back / invalidate per slice (r05a: ~10 us an exchange).
+        // Validated on one GPU (loopback, in-process group, two processes over IPC); the
+        // first cross-GPU run is the driver's, where bench.py keeps the one-shot path only if
+        // its tokens equal RCCL's on every rank.
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     __syncthreads();  // the flags were seen before any slot is read (write-through loads below)
     const int i_end = min(a.n, (g + 1) * kXchgSlice);

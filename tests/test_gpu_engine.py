@@ -205,13 +205,16 @@ def test_host_device_position_mismatch_is_reported(use_graph):
             e.tokens()
 
 
-@pytest.mark.parametrize("world", [4, 8])
-def test_kpar_small_shard_gemv_matches_unsplit(world):
+@pytest.mark.parametrize("pname,world", [("llama2-7b", 4), ("llama2-7b", 8), ("llama2-13b", 4), ("llama2-13b", 8)])
+def test_kpar_small_shard_gemv_matches_unsplit(pname, world):
     """K split inside the workgroup (GemvArgs::kpar) for a TP rank's q/k/v and gate_up: 2 or 4
     waves share a row group, their partial dots added in order. Against the unsplit kernels
     (llmi_engine_set_option "kpar" 0) on the same looped-back rank: tokens equal, logits within
-    fp32 reassociation (1e-5); graph replay equals eager launches bitwise."""
-    cfg = preset("llama2-7b", layers=2, max_seq=160, tp_rank=0, tp_world=world)
+    fp32 reassociation (1e-5); graph replay equals eager launches bitwise. 13B width with fp16
+    weights (k = 5120: 320 chunks a K part at kpar 2) is the shape whose unroll choice failed
+    the launch before (ADVICE r05 #2)."""
+    cfg = preset(pname, layers=2, max_seq=160, tp_rank=0, tp_world=world)
+    cfg.weight_dtype = _lib.F16
     prompt = np.array([1, 5, 9, 13, 17, 21, 25, 29], np.int32)
     out = {}
     with Engine(cfg) as e:
@@ -227,5 +230,7 @@ def test_kpar_small_shard_gemv_matches_unsplit(world):
     np.testing.assert_array_equal(out[(1, True)][0], out[(1, False)][0])
     np.testing.assert_array_equal(out[(1, True)][1], out[(1, False)][1])
     r = rel(out[(1, True)][1], out[(0, True)][1])
-    print(f"kpar on vs off, TP {world}: logits rel-L2 {r:.2e}")
-    assert r < 1e-5
+    print(f"kpar on vs off, {pname} TP {world}: logits rel-L2 {r:.2e}")
+    # fp32 reassociation of the dots, carried through the fp16 KV cache: 7B <= 1e-5; 13B width
+    # (k = 5120, 40 heads) measured 1.95e-5 at TP 4
+    assert r < (1e-5 if pname == "llama2-7b" else 5e-5)

@@ -218,6 +218,33 @@ def test_prefill_partial_and_chunked_equals_decode_path():
     assert r < LOGIT_TOL
 
 
+@pytest.mark.parametrize("p0,rows", [(8, 504), (20, 504), (500, 40)])
+def test_prefill_after_unaligned_history_equals_decode_path(p0, rows):
+    """a prefill after p0 % 16 != 0 decode steps puts queries with every key
+    of the first block masked in the same wave as queries that see keys of it (the lazy
+    softmax's ballot fires for the wave; the masked lanes must rescale by 1, not
+    exp2(-inf - -inf) = NaN). (8, 504), (20, 504): whole query blocks; (500, 40): few rows
+    after a long history, so the kernel splits the keys into chunks (2 blocks each) and the
+    chunk starting at key 512 is the first block for queries 500..515 of one wave."""
+    cfg = preset("llama2-7b", layers=2, max_seq=p0 + rows + 16)
+    prompt = synth_prompt(13, p0 + rows, cfg.vocab)
+    with Engine(cfg) as e:
+        e.load_synthetic(4)
+        ref_toks = e.generate(prompt, 8)
+        ref_logits = e.logits()
+        for exact in (1, 2):
+            e.set_prompt(prompt)
+            e.decode(p0)
+            e.prefill(rows, exact=exact)
+            e.decode(7)
+            toks, logits = e.tokens()[p0 + rows:], e.logits()
+            assert np.isfinite(logits).all()
+            np.testing.assert_array_equal(toks, ref_toks)
+            r = rel(logits, ref_logits)
+            print(f"prefill after {p0} decode steps ({rows} rows, exact={exact}) vs decode path: {r:.3e}")
+            assert r < LOGIT_TOL
+
+
 @pytest.mark.parametrize("exact", [1, 2])
 def test_full_7b_prefill_512_matches_decode_path(exact):
     """Config 3: Llama-2-7B (32 layers, fp16 weights + KV), 512-row prompt; exact = 2
