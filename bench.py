@@ -212,11 +212,16 @@ def prefill_side(eng, prompt_len: int = 512, reps: int = 3):
         tf = flops / best / 1e12
         # exact: hi + lo fp16 planes (2x the fp16 MFMA work); exact_fp8lo: fp16 hi + e4m3 lo
         # planes on the block-scaled fp8 MFMA (1.5x; F6 logits 1.16e-4 vs 1.14e-4 exact);
-        # fp16_activations: hi plane only
-        key = {1: "exact", 2: "exact_fp8lo", 0: "fp16_activations"}[exact]
+        # fp16_activations_approx: hi plane only -- NOT parity-qualified (its F6 logits error,
+        # 3.8e-4 at 1 layer, grows to ~2e-3 at 32 layers in the oracle study, above the north
+        # star's 1e-3): a throughput figure, labelled as such
+        key = {1: "exact", 2: "exact_fp8lo", 0: "fp16_activations_approx"}[exact]
         out[key] = {
             "ms": round(best * 1e3, 3), "tflops": round(tf, 1), "frac_of_peak": round(tf / MFMA_F16_PEAK_TFLOPS, 4),
             "mfma_work_factor": {1: 2, 2: 1.5, 0: 1}[exact]}
+        if exact == 0:
+            out[key]["parity"] = ("approximate: fp16 activations; F6 logits rel-L2 3.8e-4 (1 layer), ~2.0e-3 at 32 "
+                                  "layers (oracle study, profiles/r02_prefill_precision_study.json) vs the 1e-3 bar")
     return out
 
 

@@ -20,6 +20,8 @@ as fp32, i.e. the reference's fp32 CPU path), and records inputs + outputs:
                   greedy steps to ctx 2048 (+ the oracle's fp16-KV emulation)
   f8_ctx_history_{tiny,7b}.npz  ragged context batch with history: 3 sequences, histories
                   {0, 5, 17}, chunks {8, 4, 11}; history K/V, chunk logits + written K/V
+  f9_7b_32layers.npz  the bench model itself: Llama-2-7B shape, all 32 layers, fp32,
+                  8-token prompt, 16 greedy cached steps (tokens, first/last logits)
   tiny.npz        test_llama_run.py-like tiny model (hidden 512, 2 layers)
   manifest.json   versions + what each fixture holds
 
@@ -273,6 +275,59 @@ def gen_f8(ref, KV, c, seed, fname, hist=(0, 5, 17), lens=(8, 4, 11), new_heads=
     np.savez_compressed(os.path.join(OUT, fname), **out)
 
 
+@torch.no_grad()
+def gen_f9(ref, KV, seed=20, n_new=16):
+    """Parity at the bench's depth: the reference's LlamaForCausalLM
+    (modeling_llama.py:975-1104, 1138-1202) at the full Llama-2-7B shape, 32 layers, fp32,
+    the PRNG weights of seed 20; an 8-token prompt through the batched forward, then 15
+    greedy cached steps. ~27 GB of fp32 parameters: the module is built once (its own
+    random init) and the PRNG weights are copied in layer by layer, so no second full copy
+    of the model is ever held (the container has 62 GB)."""
+    c = LlamaConfig()
+    torch.manual_seed(0)
+    m = ref.LlamaForCausalLM(ref_config(ref, c)).eval()
+    from oracle.llama_ref import make_layer_weights
+    q, kv, I = c.q_rows, c.kv_rows, c.inter
+
+    def put(t, a):
+        t.copy_(torch.from_numpy(np.ascontiguousarray(a)).to(torch.float32))
+
+    put(m.model.embed_tokens.weight, prng.embed_fp16(seed, prng.GLOBAL_EMBED, c.vocab, c.hidden))
+    put(m.lm_head.weight, prng.linear_fp16(seed, prng.GLOBAL_LM_HEAD, c.vocab, c.hidden, 0, 0, c.hidden))
+    put(m.model.norm.weight, prng.gamma_fp16(seed, prng.GLOBAL_FINAL_NORM, c.hidden))
+    for l, layer in enumerate(m.model.layers):
+        lw = make_layer_weights(c, seed, l)
+        a = layer.self_attn
+        put(a.q_proj.weight, lw.qkv[:q])
+        put(a.k_proj.weight, lw.qkv[q:q + kv])
+        put(a.v_proj.weight, lw.qkv[q + kv:])
+        put(a.o_proj.weight, lw.o)
+        put(layer.mlp.gate_proj.weight, lw.gate_up[:I])
+        put(layer.mlp.up_proj.weight, lw.gate_up[I:])
+        put(layer.mlp.down_proj.weight, lw.down)
+        put(layer.input_layernorm.weight, lw.attn_norm)
+        put(layer.post_attention_layernorm.weight, lw.ffn_norm)
+        del lw
+    prompt = prng.prompt_ids(seed, 8, c.vocab)
+    t0 = time.perf_counter()
+    toks, first, last, _ = greedy_ref(ref, KV, m, prompt, n_new)
+    dt = time.perf_counter() - t0
+    del m
+    # the bench's fp16 KV cache, emulated by the numpy oracle (same weights, the cache's
+    # stores rounded to fp16; token-by-token like the engine's decode): what the fp16-KV
+    # engine is held to at this depth, next to its drift from the fp32 reference
+    from oracle.llama_ref import LlamaOracle
+    import gc
+    gc.collect()
+    o = LlamaOracle(c, seed=seed, kv_dtype=np.float16)
+    o_toks, o_last = o.greedy(prompt, n_new)
+    del o
+    np.savez_compressed(os.path.join(OUT, "f9_7b_32layers.npz"), seed=seed, prompt=prompt, tokens=toks,
+                        first_logits=first, last_logits=last, ref_cpu_s=dt,
+                        f16kv_tokens=np.asarray(o_toks, np.int32), f16kv_last_logits=o_last)
+    return toks
+
+
 def check():
     """Regenerate every fixture into a temporary directory and compare its arrays with
     the committed ones (timings excluded): the committed fixtures are what this script
@@ -332,6 +387,7 @@ def main(write_manifest=True):
                                                    "f8_ctx_history_tiny.npz")),
         ("f8_ctx_history_7b.npz", lambda: gen_f8(ref, KV, LlamaConfig(layers=2, max_seq=64), 19,
                                                   "f8_ctx_history_7b.npz")),
+        ("f9_7b_32layers.npz", lambda: gen_f9(ref, KV)),
     ]
     only = set(a for a in sys.argv[1:] if a.endswith(".npz"))
     for name, fn in steps:
