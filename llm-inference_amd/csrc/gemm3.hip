@@ -58,6 +58,9 @@
 #ifndef LLMI_G3_VM2
 #define LLMI_G3_VM2 1  // counted vmcnt only in j1 and j3 (0: in every phase; A/B builds only)
 #endif
+#ifndef LLMI_G3_STEADY
+#define LLMI_G3_STEADY 1  // steady-state K tiles without issue guards / runtime wait counts (0: A/B builds only)
+#endif
 #ifndef LLMI_G3_BFIRST
 #define LLMI_G3_BFIRST 1  // j0 reads B0 before A0, a scheduling barrier between (0: A first; A/B builds only)
 #endif
@@ -158,8 +161,9 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
     const unsigned lds0 = (unsigned)(uintptr_t)lds;
 
     // issue the half-image `half` (0 A0, 1 A1, 2 B0, 3 B1) of virtual K tile v
-    auto issue = [&](int v, int half) {
-        if (v >= KT) return;
+    // (GUARD false: the caller knows v < KT -- the steady-state tiles, no scalar branch)
+    auto issue = [&](int v, int half, auto guard) {
+        if (decltype(guard)::value && v >= KT) return;
         const int plane = v >= nhi ? 1 : 0;
         const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (v & 1) * kBuf + half * kHalf + w * 1024);
         // fp8 rows keep the fp16 rows' byte stride (the first half of each row is used),
@@ -236,9 +240,10 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
         bar();
     };
 
+    const std::true_type G{};  // guarded issue
     // prologue: virtual phases -6 .. -1 = A0, B0, B1, A1 of tile 0, A0, B0 of tile 1
-    issue(0, 0); issue(0, 2); issue(0, 3); issue(0, 1);
-    issue(1, 0); issue(1, 2);
+    issue(0, 0, G); issue(0, 2, G); issue(0, 3, G); issue(0, 1, G);
+    issue(1, 0, G); issue(1, 2, G);
     if (LLMI_G3_VM2)  // A0, B0, B1 of tile 0 (j0 has no wait of its own; A1 is retired by j1's)
         wait_vm(2 * (min(1, KT - 1) * 2 + 1));
     else
@@ -246,8 +251,14 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
     bar();
     if (wr == 1) bar();  // ping-pong: group 1 one barrier behind
 
-    auto ktile = [&](int kt, auto f8) {
+    // steady: kt + 2 < KT - 0 and 4 kt + 3 <= n_last, i.e. kt <= KT - 3 -- every issue is in
+    // range and the counted waits are the constants 8 (j1) and 6 (j3): no guards, no
+    // wave-uniform branch chains in the phases (LLMI_G3_STEADY; 0 = every tile generic)
+    auto ktile = [&](int kt, auto f8, auto steady) {
         constexpr bool F8 = decltype(f8)::value;
+        constexpr bool ST = decltype(steady)::value && LLMI_G3_VM2;
+        const std::integral_constant<bool, !ST> g{};
+        auto issue_g = [&](int v, int half) { issue(v, half, g); };
         const char* buf = lds + (kt & 1) * kBuf;
         const int n = 4 * kt;
         // j0: quadrant (A0, B0)
@@ -259,15 +270,16 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
             read_a(buf);
             read_b(buf + 2 * kHalf, b0);
         }
-        issue(kt + 1, 3);
+        issue_g(kt + 1, 3);
         if (LLMI_G3_VM2) bar(); else sync_reads(n);
         if constexpr (F8) mma8(acc[0][0], b0); else mma(acc[0][0], b0);
         bar();
         // j1: quadrant (A0, B1)
         read_b(buf + 3 * kHalf, b1);
-        issue(kt + 1, 1);
+        issue_g(kt + 1, 1);
         if (LLMI_G3_VM2) {  // retires A1 of tile kt (read in j2): 4 half-images issued after it
-            wait_vm(vm_count(n + 1));
+            if constexpr (ST) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else wait_vm(vm_count(n + 1));
             bar();
         } else {
             sync_reads(n + 1);
@@ -276,14 +288,15 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
         bar();
         // j2: quadrant (A1, B1)
         read_a(buf + kHalf);
-        issue(kt + 2, 0);
+        issue_g(kt + 2, 0);
         if (LLMI_G3_VM2) bar(); else sync_reads(n + 2);
         if constexpr (F8) mma8(acc[1][1], b1); else mma(acc[1][1], b1);
         bar();
         // j3: quadrant (A1, B0)
-        issue(kt + 2, 2);
+        issue_g(kt + 2, 2);
         if (LLMI_G3_VM2) {  // retires A0 / B0 and B1 of tile kt + 1 (read in its j0 / j1): 3 issued after B1
-            wait_vm(2 * max(0, min(n + 3, n_last) - n));
+            if constexpr (ST) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else wait_vm(2 * max(0, min(n + 3, n_last) - n));
             bar();
         } else {
             sync_reads(n + 3);
@@ -292,8 +305,14 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
         bar();
     };
     const int KTh = lo8 ? nhi : KT;  // fp16 K tiles (then the fp8 lo tiles)
-    for (int kt = 0; kt < KTh; ++kt) ktile(kt, std::false_type{});
-    for (int kt = KTh; kt < KT; ++kt) ktile(kt, std::true_type{});
+    const int KTs = LLMI_G3_STEADY ? KT - 2 : 0;  // tiles [0, KTs) are steady
+    const std::false_type NF{};
+    const std::true_type YF{};
+    int kt = 0;
+    for (; kt < min(KTh, KTs); ++kt) ktile(kt, NF, YF);
+    for (; kt < KTh; ++kt) ktile(kt, NF, NF);
+    for (; kt < KTs; ++kt) ktile(kt, YF, YF);
+    for (; kt < KT; ++kt) ktile(kt, YF, NF);
     if (wr == 0) bar();  // equal barrier counts
 }
 
