@@ -61,6 +61,15 @@
 #ifndef LLMI_G3_STEADY
 #define LLMI_G3_STEADY 1  // steady-state K tiles without issue guards / runtime wait counts (0: A/B builds only)
 #endif
+#ifndef LLMI_G3_SBASE
+#define LLMI_G3_SBASE 1  // the copies' K offset in the scalar base, not a per-lane add (0: A/B builds only)
+#endif
+#ifndef LLMI_G3_PAIR
+#define LLMI_G3_PAIR 1  // steady tiles in pairs with a compile-time buffer parity (0: A/B builds only)
+#endif
+#ifndef LLMI_G3_PAIR_SK
+#define LLMI_G3_PAIR_SK 1  // stream-K: the owner's piece paired (the later-piece site stays generic: both paired spill)
+#endif
 #ifndef LLMI_G3_BFIRST
 #define LLMI_G3_BFIRST 1  // j0 reads B0 before A0, a scheduling barrier between (0: A first; A/B builds only)
 #endif
@@ -124,7 +133,10 @@ __device__ __forceinline__ float silu3(float v) { return v / (1.0f + expf(-v)); 
 // tiles; both 128 B per LDS row). nhi + nlo >= 2: the prologue's counted wait covers the
 // first two tiles. Every wave passes the same barriers, and every LDS read has retired on
 // return, so the caller may reuse the LDS.
-template <int EPI>
+// PAIRED: steady tiles in (even, odd) pairs with a compile-time buffer parity -- only in the
+// plain gemm3_kernel: in the stream-K and balanced kernels the duplicated tile bodies push the
+// allocator past 256 VGPRs (10-15 spilled)
+template <int EPI, bool PAIRED = false>
 __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, int ct, int hi0, int nhi, int lo0,
                                        int nlo, f4v (&acc)[2][2][4][2]) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -162,19 +174,29 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
 
     // issue the half-image `half` (0 A0, 1 A1, 2 B0, 3 B1) of virtual K tile v
     // (GUARD false: the caller knows v < KT -- the steady-state tiles, no scalar branch)
-    auto issue = [&](int v, int half, auto guard) {
+    // vpar: v & 1 when the caller knows it at compile time (std::integral_constant), else
+    // an int; the LDS destination then folds to a constant
+    auto issue = [&](int v, int half, auto guard, auto vpar) {
         if (decltype(guard)::value && v >= KT) return;
         const int plane = v >= nhi ? 1 : 0;
-        const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (v & 1) * kBuf + half * kHalf + w * 1024);
+        const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (int)vpar * kBuf + half * kHalf + w * 1024);
         // fp8 rows keep the fp16 rows' byte stride (the first half of each row is used),
         // so the per-thread offsets serve both passes -- no second set of registers
         const unsigned k0b = (unsigned)(plane ? lo0 + v - nhi : hi0 + v) * 128u;
         const char* base = half < 2 ? abase[plane] : (lo8 && plane) ? w8base : wbase;  // uniform
+#if LLMI_G3_SBASE
+        // the K offset (and W half 1's row offset) go into the scalar base: the per-lane
+        // offsets are the loop-invariant a_off / b_off, no VALU add per copy
+        const char* sb = base + k0b + (half == 3 ? b_half1 : 0u);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) glds_s(sb, half < 2 ? a_off[half][i] : b_off[i], dst + i * kT * 16);
+#else
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const unsigned off = half < 2 ? a_off[half][i] + k0b : b_off[i] + (half == 3 ? b_half1 : 0u) + k0b;
             glds_s(base, off, dst + i * kT * 16);
         }
+#endif
     };
     // phase n issues: j0 B1 of t+1, j1 A1 of t+1, j2 A0 of t+2, j3 B0 of t+2 (t = n >> 2)
     const int n_last = 4 * (KT - 2) + 1;  // last phase whose issue is in range
@@ -241,9 +263,11 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
     };
 
     const std::true_type G{};  // guarded issue
+    const std::integral_constant<int, 0> P0{};
+    const std::integral_constant<int, 1> P1{};
     // prologue: virtual phases -6 .. -1 = A0, B0, B1, A1 of tile 0, A0, B0 of tile 1
-    issue(0, 0, G); issue(0, 2, G); issue(0, 3, G); issue(0, 1, G);
-    issue(1, 0, G); issue(1, 2, G);
+    issue(0, 0, G, P0); issue(0, 2, G, P0); issue(0, 3, G, P0); issue(0, 1, G, P0);
+    issue(1, 0, G, P1); issue(1, 2, G, P1);
     if (LLMI_G3_VM2)  // A0, B0, B1 of tile 0 (j0 has no wait of its own; A1 is retired by j1's)
         wait_vm(2 * (min(1, KT - 1) * 2 + 1));
     else
@@ -254,12 +278,18 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
     // steady: kt + 2 < KT - 0 and 4 kt + 3 <= n_last, i.e. kt <= KT - 3 -- every issue is in
     // range and the counted waits are the constants 8 (j1) and 6 (j3): no guards, no
     // wave-uniform branch chains in the phases (LLMI_G3_STEADY; 0 = every tile generic)
-    auto ktile = [&](int kt, auto f8, auto steady) {
+    // par: kt & 1, a compile-time constant in the paired steady loop (LLMI_G3_PAIR), so the
+    // LDS read and copy addresses of the tile's buffer fold to immediate offsets
+    auto ktile = [&](int kt, auto f8, auto steady, auto par) {
         constexpr bool F8 = decltype(f8)::value;
         constexpr bool ST = decltype(steady)::value && LLMI_G3_VM2;
         const std::integral_constant<bool, !ST> g{};
-        auto issue_g = [&](int v, int half) { issue(v, half, g); };
-        const char* buf = lds + (kt & 1) * kBuf;
+        auto issue_g = [&](int v, int half) {
+            if constexpr (std::is_same_v<decltype(par), int>) issue(v, half, g, v & 1);
+            else if ((v - kt) & 1) issue(v, half, g, std::integral_constant<int, 1 - decltype(par)::value>{});
+            else issue(v, half, g, par);
+        };
+        const char* buf = lds + (int)par * kBuf;
         const int n = 4 * kt;
         // j0: quadrant (A0, B0)
         if (LLMI_G3_BFIRST) {
@@ -309,10 +339,25 @@ __device__ __forceinline__ void g3_run(const Gemm2Args& a, char* lds, int m0, in
     const std::false_type NF{};
     const std::true_type YF{};
     int kt = 0;
-    for (; kt < min(KTh, KTs); ++kt) ktile(kt, NF, YF);
-    for (; kt < KTh; ++kt) ktile(kt, NF, NF);
-    for (; kt < KTs; ++kt) ktile(kt, YF, YF);
-    for (; kt < KT; ++kt) ktile(kt, YF, NF);
+    if (PAIRED) {  // steady tiles in (even, odd) pairs: static buffer parity
+        for (; kt + 1 < min(KTh, KTs); kt += 2) {
+            ktile(kt, NF, YF, P0);
+            ktile(kt + 1, NF, YF, P1);
+        }
+    }
+    for (; kt < min(KTh, KTs); ++kt) ktile(kt, NF, YF, kt & 1);
+    for (; kt < KTh; ++kt) ktile(kt, NF, NF, kt & 1);
+    if (PAIRED && (kt & 1)) {  // the fp8 pass may start on an odd tile
+        if (kt < KTs) { ktile(kt, YF, YF, P1); ++kt; }
+    }
+    if (PAIRED) {
+        for (; kt + 1 < KTs; kt += 2) {
+            ktile(kt, YF, YF, P0);
+            ktile(kt + 1, YF, YF, P1);
+        }
+    }
+    for (; kt < KTs; ++kt) ktile(kt, YF, YF, kt & 1);
+    for (; kt < KT; ++kt) ktile(kt, YF, NF, kt & 1);
     if (wr == 0) bar();  // equal barrier counts
 }
 
@@ -437,7 +482,8 @@ __global__ __launch_bounds__(kT) void gemm3_kernel(Gemm2Args a) {
     const int KTs = (lo8 ? 2 : 1) * ((slice + 1) * KT_all / S) - kt0;  // 64-deep K tiles per plane in this slice
     f4v acc[2][2][4][2];
     zero_acc(acc);
-    g3_run<EPI>(a, lds, m0, ct, kt0, KTs, lo8 ? kt0 / 2 : kt0, lo8 ? KTs / 2 : (a.planes == 2 ? KTs : 0), acc);
+    g3_run<EPI, LLMI_G3_PAIR != 0>(a, lds, m0, ct, kt0, KTs, lo8 ? kt0 / 2 : kt0, lo8 ? KTs / 2 : (a.planes == 2 ? KTs : 0),
+                                   acc);
     g3_epilogue<EPI>(a, lds, acc, m0, ct, slice);
 }
 
@@ -628,7 +674,7 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
         const int owner = sk_wg_of((long)ct * d.U2, TPs, Gp);  // in units of sibling groups
         if (s > 0) {  // a later piece of the tile: slot v - owner - 1, then its flag
             zero_acc(acc);
-            g3_run<EPI>(a, lds, m0, ct, vs, nhi, lo0, nlo, acc);
+            g3_run<EPI, false>(a, lds, m0, ct, vs, nhi, lo0, nlo, acc);
             const int sl = v - owner - 1;
             // payload written through (sc1) by buffer stores: one SGPR offset per quadrant
             // instead of 32 64-bit addresses, and no release fence (guide R1 hand-off)
@@ -655,7 +701,7 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
             }
         } else {
             zero_acc(acc);
-            g3_run<EPI>(a, lds, m0, ct, 0, nhi, lo0, nlo, acc);  // a tile's head: from K tile 0
+            g3_run<EPI, LLMI_G3_PAIR_SK != 0>(a, lds, m0, ct, 0, nhi, lo0, nlo, acc);  // a tile's head: from K tile 0
             const int np = LLMI_SK_EXP == 2 ? 0 : sk_wg_of((long)ct * d.U2 + d.U2 - 1, TPs, Gp) - v;  // later pieces
             if (np > 0) {
                 if (t == 0) {
