@@ -67,9 +67,6 @@
 #ifndef LLMI_G3_PAIR
 #define LLMI_G3_PAIR 1  // steady tiles in pairs with a compile-time buffer parity (0: A/B builds only)
 #endif
-#ifndef LLMI_G3_PAIR_SK
-#define LLMI_G3_PAIR_SK 1  // stream-K: the owner's piece paired (the later-piece site stays generic: both paired spill)
-#endif
 #ifndef LLMI_G3_BFIRST
 #define LLMI_G3_BFIRST 1  // j0 reads B0 before A0, a scheduling barrier between (0: A first; A/B builds only)
 #endif
@@ -674,7 +671,7 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
         const int owner = sk_wg_of((long)ct * d.U2, TPs, Gp);  // in units of sibling groups
         if (s > 0) {  // a later piece of the tile: slot v - owner - 1, then its flag
             zero_acc(acc);
-            g3_run<EPI, false>(a, lds, m0, ct, vs, nhi, lo0, nlo, acc);
+            g3_run<EPI>(a, lds, m0, ct, vs, nhi, lo0, nlo, acc);
             const int sl = v - owner - 1;
             // payload written through (sc1) by buffer stores: one SGPR offset per quadrant
             // instead of 32 64-bit addresses, and no release fence (guide R1 hand-off)
@@ -701,7 +698,7 @@ __global__ __launch_bounds__(kT) void gemm3_sk_kernel(Gemm2Args a) {
             }
         } else {
             zero_acc(acc);
-            g3_run<EPI, LLMI_G3_PAIR_SK != 0>(a, lds, m0, ct, 0, nhi, lo0, nlo, acc);  // a tile's head: from K tile 0
+            g3_run<EPI>(a, lds, m0, ct, 0, nhi, lo0, nlo, acc);  // a tile's head: from K tile 0
             const int np = LLMI_SK_EXP == 2 ? 0 : sk_wg_of((long)ct * d.U2 + d.U2 - 1, TPs, Gp) - v;  // later pieces
             if (np > 0) {
                 if (t == 0) {
