@@ -7,7 +7,7 @@
 #   bench             bench.py (BENCH_ARGS env: extra flags)
 #   trace             rocprofv3 kernel trace of one eager bench step (+ tools/trace_summary.py)
 #   pmc               FETCH_SIZE and WRITE_SIZE passes (separate runs) on the decode kernels
-#   pftrace           rocprofv3 kernel trace of a 512-row prefill (PF_MODE env: prefill_probe mode, default 2)
+#   pftrace           rocprofv3 kernel trace of a 512-row prefill (PF_MODE env: exact | exact8 | fast, default exact8)
 #   mfma              MFMA-busy PMC pass on the prefill GEMMs / attention
 #   cmd=<command>     any other command, under a 600-s limit, output in gpurun_out/cmd_<tag>_<n>.log
 # Every output lands in gpurun_out/<step>_<tag>.*; copy what is judged into profiles/.
@@ -59,17 +59,17 @@ for s in "$@"; do
         find /tmp/pmc_$c -name '*counter_collection.csv' -exec cp {} $OUT/pmc_${c}_$TAG.csv \;
       done ;;
     pftrace)
-      step "kernel trace (prefill, mode ${PF_MODE:-2})"
+      step "kernel trace (prefill, mode ${PF_MODE:-exact8})"
       rm -rf /tmp/prof_pf
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_pf -o pf --output-format csv -- \
-        python3 tools/prefill_probe.py 512 ${PF_MODE:-2} > $OUT/pftrace_$TAG.log 2>&1 || fail $? pftrace $OUT/pftrace_$TAG.log
+        python3 tools/prefill_probe.py 512 3 ${PF_MODE:-exact8} > $OUT/pftrace_$TAG.log 2>&1 || fail $? pftrace $OUT/pftrace_$TAG.log
       find /tmp/prof_pf -name '*kernel_stats.csv' -exec cp {} $OUT/prefill_kernel_stats_$TAG.csv \; ;;
     mfma)
       step "pmc mfma (prefill)"
       rm -rf /tmp/pmc_m
       timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE \
         --kernel-include-regex 'gemm[23]?_(sk_)?kernel|attn_prefill' -d /tmp/pmc_m -o pmc --output-format csv -- \
-        python3 tools/prefill_probe.py 512 ${PF_MODE:-1} > $OUT/mfma_$TAG.log 2>&1 || fail $? mfma $OUT/mfma_$TAG.log
+        python3 tools/prefill_probe.py 512 3 ${PF_MODE:-exact} > $OUT/mfma_$TAG.log 2>&1 || fail $? mfma $OUT/mfma_$TAG.log
       find /tmp/pmc_m -name '*counter_collection.csv' -exec cp {} $OUT/pmc_mfma_$TAG.csv \; ;;
     cmd=*)
       c=${s#cmd=}
