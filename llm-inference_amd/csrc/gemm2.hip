@@ -633,6 +633,10 @@ bool sk_setup(Gemm2Args& g, hipStream_t s) {
         return e && std::string(e) == "0";
     }();
     if (off) return false;
+    // one fp16 plane (the fp16-activation prefill): since the plain kernel's steady tiles run
+    // paired (gemm3.hip, round 6) it is the faster form -- 512-row prefill 9.37-9.41 -> 9.17-9.18
+    // ms on one box, while two planes and fp8 lo planes stay faster on stream-K (r06m)
+    if (g.planes == 1 && !g.lo8) return false;
     const int n_cu = cu_count();
     const Gemm3SkPlan p = gemm3_sk_plan(g.m, g.n, g.k, g.epi, g.planes, g.lo8, n_cu);
     if (p.pmax < 1 || p.pmax > 3) return false;
