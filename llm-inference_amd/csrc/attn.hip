@@ -103,6 +103,19 @@ __global__ __launch_bounds__(kThreads) void attn_oproj_kernel(OprojArgs a, int n
     xchg_detail::xchg_tail(a.xt, a.xt_cnt, reinterpret_cast<int*>(smem));  // TP: push xacc from this launch
 }
 
+// two heads per workgroup (oproj_body2)
+template <typename WT, int NPL>
+__global__ __launch_bounds__(kThreads) void attn_oproj2_kernel(OprojArgs a, int ns) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    WgStamp ts(a.stamps);
+    oproj_body2<WT, NPL, PlainIO>(a, blockIdx.x, blockIdx.y, ns, smem);
+    xchg_detail::xchg_tail(a.xt, a.xt_cnt, reinterpret_cast<int*>(smem));  // TP: push xacc from this launch
+}
+
+#ifndef LLMI_OPROJ_HG
+#define LLMI_OPROJ_HG 2  // heads per fp16 o_proj workgroup when the head count is even (1: one head, A/B)
+#endif
+
 int oproj_npl(const OprojArgs& a) {
     const long target = (long)a.heads * a.n_rows / (1024 * 16);  // ~1024 workgroups
 #ifdef LLMI_OPROJ_NPL
@@ -116,6 +129,15 @@ int oproj_launch_w(const OprojArgs& a, hipStream_t s) {
     // ~1024 workgroups: rows per workgroup = 16 * NPL
     const int ns = (a.max_seq + CH - 1) / CH;
     const int npl = oproj_npl(a);
+    // fp16 weights only: the int8 form needs 92 VGPRs with two heads (68 with one), so 13B's
+    // 1,600 workgroups no longer fit in one round and it measured 0.7-0.9 us slower (r06q); fp32
+    // weights (the parity instantiation) would need 140
+    if (LLMI_OPROJ_HG == 2 && sizeof(WT) == 2 && a.heads % 2 == 0 && !a.head_major && npl == 8) {
+        const dim3 grid2(a.heads / 2, (a.n_rows + 8 * npl - 1) / (8 * npl));
+        hipLaunchKernelGGL((attn_oproj2_kernel<WT, 8>), grid2, dim3(kThreads), oproj2_lds<8>(), s, a, ns);
+        LLMI_HIP(hipGetLastError());
+        return LLMI_OK;
+    }
     const dim3 grid(a.heads, (a.n_rows + 16 * npl - 1) / (16 * npl));
     switch (npl) {
 #if LLMI_OPROJ_NPL == 16

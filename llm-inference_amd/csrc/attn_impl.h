@@ -531,5 +531,161 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
 }
 
 
+// Two heads per workgroup (LLMI_OPROJ_HG 2, an even head count): workgroup (head pair hp,
+// row chunk of 8 * NPL rows). 16-lane groups 0-7 take head 2 hp, 8-15 head 2 hp + 1, each on
+// the same NPL rows (row0 + (grp & 7) + 8 t), so a row's two head products meet in LDS and go
+// out as ONE atomic of fixed(y_a) + fixed(y_b): the integer sum of the two atomics it replaces,
+// so xacc is bitwise that of oproj_body, with half the atomic write traffic (512 KB at 7B).
+// W_o bytes per workgroup (32 KB at NPL 8) and the workgroup count stay those of oproj_body;
+// the merge is one thread per (head, dim) over every split.
+template <int NPL>
+constexpr size_t oproj2_lds() { return (4 * kMaxSplits + 4 + 2 * D + 2 * 8 * NPL) * sizeof(float); }
+
+template <typename WT, int NPL, typename IO>
+__device__ __forceinline__ void oproj_body2(const OprojArgs& a, int hp, int chunk, int ns, float* smem) {
+    float* m_s = smem;                      // [2][kMaxSplits]
+    float* l_s = m_s + 2 * kMaxSplits;      // [2][kMaxSplits]
+    float* linv_s = l_s + 2 * kMaxSplits;   // [2] (+2 pad)
+    float* o_s = linv_s + 4;                // [2][D] merged outputs
+    float* y_s = o_s + 2 * D;               // [2][8 * NPL] per-head row products
+    const int tid = threadIdx.x;
+    const int grp = tid / LPR, l16 = tid % LPR;
+    const int hs = grp >> 3, g8 = grp & 7;  // this group's head (of the pair) and row lane
+    const int h = 2 * hp + hs;
+    const int row0 = chunk * 8 * NPL;
+    const WT* w = reinterpret_cast<const WT*>(a.w);
+
+    Ws ws = ws_carve(const_cast<void*>(a.workspace), a.heads, ns);
+    const int mh = tid >> 7, d = tid & (D - 1);  // merge: thread (head mh of the pair, dim d)
+    const float* mlh = ws.ml + (size_t)(2 * hp + mh) * ns * 2;
+    const float* oh = ws.o + (size_t)(2 * hp + mh) * ns * D + d;
+    constexpr int kOv = 2 * kMergeChunk;
+    float ov[kOv];
+    const int nl = a.nact > 0 ? min(a.nact, ns) : ns;
+    // issue order as oproj_body: partials, (m, l), then the W_o slices, before any wait
+#pragma unroll
+    for (int i = 0; i < kOv; ++i) ov[i] = IO::ld(oh + (size_t)(i < nl ? i : 0) * D);
+    constexpr int kMlPer = kMaxSplits / (kThreads / 2);
+    float mr[kMlPer], lr[kMlPer];
+#pragma unroll
+    for (int i = 0; i < kMlPer; ++i) {
+        if (i * (kThreads / 2) < nl) {
+            const int sp = min(d + i * (kThreads / 2), nl - 1);
+            mr[i] = IO::ld(mlh + 2 * sp);
+            lr[i] = IO::ld(mlh + 2 * sp + 1);
+        }
+    }
+    W8<WT> wr[NPL];
+#pragma unroll
+    for (int t = 0; t < NPL; ++t) {
+        int row = row0 + g8 + 8 * t;
+        row = row < a.n_rows ? row : a.n_rows - 1;
+        if constexpr (sizeof(WT) == 1 && NPL >= 2) {
+            if (t < NPL / 2) {  // int8: two rows per 16-lane group, 8 lanes each (as oproj_load_w)
+                int r2 = row0 + g8 + 8 * (2 * t + (l16 >> 3));
+                r2 = r2 < a.n_rows ? r2 : a.n_rows - 1;
+                wr[t].v[0] = ld_nt16(w + (size_t)r2 * a.ldw + (size_t)h * D + (l16 & 7) * 16);
+            }
+        } else {
+            wr[t] = ld_w8<WT>(w + (size_t)row * a.ldw + (size_t)h * D + l16 * 8);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kMlPer; ++i) {
+        const int sp = d + i * (kThreads / 2);
+        if (i * (kThreads / 2) < nl && sp < nl) {
+            m_s[mh * kMaxSplits + sp] = mr[i];
+            l_s[mh * kMaxSplits + sp] = lr[i];
+        }
+    }
+    int nact = nl;
+    if (a.nact <= 0) {
+        const int pos = a.pos_dev ? *a.pos_dev : a.pos_host;
+        if (pos < 0 || pos >= a.max_seq) return;
+        nact = (pos + 1 + CH - 1) / CH;
+    }
+    __syncthreads();
+    // log-sum-exp weights: wave 0 for head 0 of the pair, wave 2 for head 1
+    if ((tid & (D - 1)) < kWave) {
+        float* mw = m_s + mh * kMaxSplits;
+        const float* lw = l_s + mh * kMaxSplits;
+        const int ln = tid & (kWave - 1);
+        float M = -INFINITY;
+        for (int sp = ln; sp < nact; sp += kWave) M = fmaxf(M, mw[sp]);
+        M = wave_max(M);
+        float lsum = 0.f;
+        for (int sp = ln; sp < nact; sp += kWave) {
+            const float wgt = expf(mw[sp] - M);
+            mw[sp] = wgt;
+            lsum = fmaf(lw[sp], wgt, lsum);
+        }
+        lsum = wave_sum(lsum);
+        if (ln == 0) linv_s[mh] = 1.0f / lsum;
+    }
+    __syncthreads();
+    {
+        // the same two interleaved partial sums (even / odd splits) oproj_body's two
+        // threads per dim form, added in the same order: bitwise its merged output
+        const float* mw = m_s + mh * kMaxSplits;
+        float O0 = 0.f, O1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < kMergeChunk; ++i) {
+            const int s0 = 2 * i, s1 = 2 * i + 1;
+            O0 = fmaf(s0 < nact ? ov[s0] : 0.f, s0 < nact ? mw[s0] : 0.f, O0);
+            O1 = fmaf(s1 < nact ? ov[s1] : 0.f, s1 < nact ? mw[s1] : 0.f, O1);
+        }
+        for (int sp = kOv; sp < nact; sp += 2) {
+            O0 = fmaf(IO::ld(oh + (size_t)sp * D), mw[sp], O0);
+            if (sp + 1 < nact) O1 = fmaf(IO::ld(oh + (size_t)(sp + 1) * D), mw[sp + 1], O1);
+        }
+        o_s[mh * D + d] = (O0 + O1) * linv_s[mh];
+    }
+    __syncthreads();
+    float* yh = y_s + hs * 8 * NPL;
+    const float* oh_s = o_s + hs * D;
+    if constexpr (sizeof(WT) == 1 && NPL >= 2) {
+        float x16[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x16[i] = oh_s[(l16 & 7) * 16 + i];
+#pragma unroll
+        for (int u = 0; u < NPL / 2; ++u) {
+            const uint32_t q[4] = {wr[u].v[0].x, wr[u].v[0].y, wr[u].v[0].z, wr[u].v[0].w};
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc = fmaf((float)(int8_t)((q[i / 4] >> (8 * (i % 4))) & 0xff), x16[i], acc);
+            acc = oct8_sum(acc);
+            if ((l16 & 7) == 0) yh[g8 + 8 * (2 * u + (l16 >> 3))] = acc;
+        }
+    } else {
+        float xv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[i] = oh_s[l16 * 8 + i];
+#pragma unroll
+        for (int t = 0; t < NPL; ++t) {
+            float wv[8];
+            unpack_w8<WT>(wr[t], wv);
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc = fmaf(wv[i], xv[i], acc);
+            acc = row16_sum(acc);
+            if (l16 == 0) yh[g8 + 8 * t] = acc;
+        }
+    }
+    __syncthreads();
+    if (tid < 8 * NPL) {
+        const int row = row0 + tid;
+        if (row < a.n_rows) {
+            float va = y_s[tid], vb = y_s[8 * NPL + tid];
+            if (a.scales) {
+                const float sc = __half2float(a.scales[row]);
+                va *= sc;
+                vb *= sc;
+            }
+            atomicAdd(reinterpret_cast<unsigned long long*>(a.xacc + row),
+                      (unsigned long long)(to_fixed(va) + to_fixed(vb)));
+        }
+    }
+}
+
 }  // namespace attn_detail
 }  // namespace llmi

@@ -37,7 +37,7 @@ def role(name):
         return "down"
     if "attn_decode_kernel<__half>" in name or "attn_decode_kernel<__half, " in name:
         return "attn"
-    if "attn_oproj_kernel<__half" in name:
+    if "attn_oproj_kernel<__half" in name or "attn_oproj2_kernel<__half" in name:
         return "o"
     return None
 
