@@ -98,6 +98,10 @@ struct StepGraphs {
     }
 };
 
+#ifndef LLMI_DOWN_STORE
+#define LLMI_DOWN_STORE 1  // unsplit down: rows written as xmid + fixed(y), not seeded + atomically added (0: A/B)
+#endif
+
 struct Engine {
     llmi_config c{};
     int device = 0;
@@ -685,9 +689,12 @@ struct Engine {
         a.w = L.gu; a.scales = L.gu_s; a.w_dtype = wdt;
         a.n_rows = 2 * il; a.k = c.hidden;
         a.x_fixed = xacc; a.x_out = x;  // residual after attention, written back to x by workgroup 0
-        // hand the mid-layer residual to the layer output accumulator (rank 0 carries it)
-        a.seed_src = xacc; a.seed_dst = res[(l + 1) % 2]; a.seed_n = c.hidden;
-        a.seed_keep = c.tp_rank == 0 ? 1 : 0;
+        // hand the mid-layer residual to the layer output accumulator (rank 0 carries it) --
+        // unless the down GEMV writes each output row itself (down_single)
+        if (!down_single()) {
+            a.seed_src = xacc; a.seed_dst = res[(l + 1) % 2]; a.seed_n = c.hidden;
+            a.seed_keep = c.tp_rank == 0 ? 1 : 0;
+        }
         a.gamma = L.ffn_norm; a.g_dtype = edt; a.eps = c.rms_eps;
         a.epi = EPI_SILU_MUL; a.pair_off = il; a.y = act;
         a.kpar = kpar_of(il);
@@ -702,11 +709,20 @@ struct Engine {
         a.epi = EPI_ATOMIC; a.yacc = res[(l + 1) % 2];
         // int8 rows are half the bytes of fp16 ones: K slices keep the loads per row in
         // flight and the x image per workgroup small (exact: int64 atomics)
-        a.ksplit = (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT
-                   : (wdt == LLMI_F16 && il % (8 * LLMI_F16_DOWN_KSPLIT) == 0) ? LLMI_F16_DOWN_KSPLIT
-                                                                               : 1;
+        a.ksplit = down_ksplit();
+        if (down_single()) {  // one producer per row: x_{l+1}[r] = xmid[r] + fixed(down_r), no seed, no atomic
+            a.yacc_single = 1;
+            a.yacc_base = c.tp_rank == 0 ? xacc : nullptr;  // the other TP ranks carry no residual
+        }
         return a;
     }
+    int down_ksplit() const {
+        return (wdt == LLMI_I8 && il % (16 * LLMI_I8_DOWN_KSPLIT) == 0) ? LLMI_I8_DOWN_KSPLIT
+               : (wdt == LLMI_F16 && il % (8 * LLMI_F16_DOWN_KSPLIT) == 0) ? LLMI_F16_DOWN_KSPLIT
+                                                                           : 1;
+    }
+    // the down GEMV writes its rows itself (LLMI_DOWN_STORE; round 6) when K is not split
+    bool down_single() const { return LLMI_DOWN_STORE && down_ksplit() == 1; }
 
 
     // One token = start, L x (attention phase | reduce xacc, ffn phase | reduce x),

@@ -240,6 +240,18 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
     }
 
     unsigned long long best = 0ull;
+    // single-producer EPI_ATOMIC: the first group's base values, loaded with the prologue so the
+    // epilogue's store does not wait for them (lane r holds row rows0[r])
+    long long pre_b = 0;
+    if constexpr (EPI == EPI_ATOMIC) {
+        if (a.yacc_single && a.yacc_base && lane < ROWS && g0 < n_groups)
+        {
+            int rr = rows0[0];
+#pragma unroll
+            for (int r = 1; r < ROWS; ++r) rr = lane == r ? rows0[r] : rr;  // no dynamic register index
+            pre_b = IO::ld_ll(a.yacc_base + min(rr, a.n_rows - 1));
+        }
+    }
     auto finish = [&](int g, const int* rows, float* acc) {
         if constexpr (KP > 1) {  // the K parts of one group meet in LDS; part 0 adds them in order
 #pragma unroll
@@ -273,8 +285,15 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
                 if (lane == r) {
                     float v = acc[r];
                     if (EPI == EPI_ATOMIC) {
-                        atomicAdd(reinterpret_cast<unsigned long long*>(a.yacc + row),
-                                  (unsigned long long)to_fixed(v));
+                        if (a.yacc_single) {  // single producer: base + fixed(v), written through (sc1)
+                            const long long b = !a.yacc_base ? 0ll : g == g0 ? pre_b : IO::ld_ll(a.yacc_base + row);
+                            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.yacc + row),
+                                               (unsigned long long)(b + to_fixed(v)), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        } else {
+                            atomicAdd(reinterpret_cast<unsigned long long*>(a.yacc + row),
+                                      (unsigned long long)to_fixed(v));
+                        }
                     } else {
                         if (EPI == EPI_ADD) v += a.resid_scale * IO::ld(a.resid + row);
                         IO::st(a.y + row, v);

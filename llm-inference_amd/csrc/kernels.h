@@ -62,6 +62,11 @@ struct GemvArgs {
     int ldw = 0;                   // row stride of W in elements (0: k)
     int ksplit = 1;                // EPI_ATOMIC: K split over ksplit workgroups (k % (ksplit * 16 B) == 0)
     long long* yacc = nullptr;     // EPI_ATOMIC target
+    // EPI_ATOMIC with ksplit 1 and yacc_single set: every row has ONE producer, so the row is
+    // written (write-through) as yacc_base[r] + fixed(acc) (yacc_base null: fixed(acc) alone)
+    // instead of an atomic add into a seeded yacc -- the same integer, no seed pass, no atomic
+    int yacc_single = 0;
+    const long long* yacc_base = nullptr;
     // residual hand-over: the workgroups copy seed_src[0..seed_n) (or zeros when !seed_keep)
     // to seed_dst, one slice each (the next fixed-point accumulator's starting value)
     const long long* seed_src = nullptr;
