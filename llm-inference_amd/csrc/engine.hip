@@ -98,6 +98,9 @@ struct StepGraphs {
     }
 };
 
+#ifndef LLMI_SEED_FROM_DOWN
+#define LLMI_SEED_FROM_DOWN 1  // single rank: down seeds the next o_proj sum; the attention writes no seed (0: A/B)
+#endif
 #ifndef LLMI_DOWN_STORE
 #define LLMI_DOWN_STORE 1  // unsplit down: rows written as xmid + fixed(y), not seeded + atomically added (0: A/B)
 #endif
@@ -667,6 +670,7 @@ struct Engine {
         a.out = attn_out; a.workspace = attn_ws;
         a.nact = rec_nact;
         a.err = &st->error;
+        if (l > 0 && seed_from_down()) a.xacc = nullptr;  // layer l - 1's down seeded xacc already
         return a;
     }
     OprojArgs o_args(int l) const {
@@ -713,6 +717,9 @@ struct Engine {
         if (down_single()) {  // one producer per row: x_{l+1}[r] = xmid[r] + fixed(down_r), no seed, no atomic
             a.yacc_single = 1;
             a.yacc_base = c.tp_rank == 0 ? xacc : nullptr;  // the other TP ranks carry no residual
+            // single rank: the same row also seeds the next layer's o_proj sum (xacc), so that
+            // layer's attention writes no seed (seed_from_down)
+            if (seed_from_down()) a.yacc_copy = xacc;
         }
         return a;
     }
@@ -723,6 +730,9 @@ struct Engine {
     }
     // the down GEMV writes its rows itself (LLMI_DOWN_STORE; round 6) when K is not split
     bool down_single() const { return LLMI_DOWN_STORE && down_ksplit() == 1; }
+    // ... and on a single rank also the next layer's o_proj seed (with TP the seed must be the
+    // all-reduced residual, which only exists after the exchange)
+    bool seed_from_down() const { return LLMI_SEED_FROM_DOWN && down_single() && c.tp_world == 1 && !grouped; }
 
 
     // One token = start, L x (attention phase | reduce xacc, ffn phase | reduce x),

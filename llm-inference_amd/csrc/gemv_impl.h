@@ -287,9 +287,12 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
                     if (EPI == EPI_ATOMIC) {
                         if (a.yacc_single) {  // single producer: base + fixed(v), written through (sc1)
                             const long long b = !a.yacc_base ? 0ll : g == g0 ? pre_b : IO::ld_ll(a.yacc_base + row);
-                            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.yacc + row),
-                                               (unsigned long long)(b + to_fixed(v)), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+                            const unsigned long long nv = (unsigned long long)(b + to_fixed(v));
+                            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.yacc + row), nv,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (a.yacc_copy)  // this row's xmid was read above (pre_b): overwriting it is safe
+                                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.yacc_copy + row), nv,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         } else {
                             atomicAdd(reinterpret_cast<unsigned long long*>(a.yacc + row),
                                       (unsigned long long)to_fixed(v));

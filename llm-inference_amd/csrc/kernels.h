@@ -67,6 +67,7 @@ struct GemvArgs {
     // instead of an atomic add into a seeded yacc -- the same integer, no seed pass, no atomic
     int yacc_single = 0;
     const long long* yacc_base = nullptr;
+    long long* yacc_copy = nullptr;  // yacc_single: the same value also written here (next o_proj's seed)
     // residual hand-over: the workgroups copy seed_src[0..seed_n) (or zeros when !seed_keep)
     // to seed_dst, one slice each (the next fixed-point accumulator's starting value)
     const long long* seed_src = nullptr;
