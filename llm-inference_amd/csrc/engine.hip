@@ -98,6 +98,9 @@ struct StepGraphs {
     }
 };
 
+#ifndef LLMI_GU_XOUT
+#define LLMI_GU_XOUT 0
+#endif
 #ifndef LLMI_SEED_FROM_DOWN
 #define LLMI_SEED_FROM_DOWN 1  // single rank: down seeds the next o_proj sum; the attention writes no seed (0: A/B)
 #endif
@@ -692,7 +695,11 @@ struct Engine {
         a.stamps = stamp_ptr();
         a.w = L.gu; a.scales = L.gu_s; a.w_dtype = wdt;
         a.n_rows = 2 * il; a.k = c.hidden;
-        a.x_fixed = xacc; a.x_out = x;  // residual after attention, written back to x by workgroup 0
+        a.x_fixed = xacc;  // residual after attention (fixed point)
+        // (no fp32 copy into x here: the lm_head launch writes the final hidden state there, and
+        // nothing reads a mid-layer copy -- it was 16 KB of stores on workgroup 0 every layer;
+        // LLMI_GU_XOUT=1 restores it for A/B)
+        if (LLMI_GU_XOUT) a.x_out = x;
         // hand the mid-layer residual to the layer output accumulator (rank 0 carries it) --
         // unless the down GEMV writes each output row itself (down_single)
         if (!down_single()) {
