@@ -155,9 +155,20 @@ constexpr size_t kAttnLds = (3 * D + CH + (kThreads / LPR) * D + 4) * sizeof(flo
 // loads are issued from the kernel arguments alone, before the device position (a
 // scalar load from memory another kernel just wrote) has arrived; rows past the
 // position are loaded (valid cache memory below max_seq) and ignored.
-template <typename KT, typename IO, bool HOST_SIZED = false>
+// agent-scope (sc1: L1 bypassed) 8-byte granule load, the fused q/k/v launch's hand-off
+__device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// TAGGED (fused q/k/v + attention launch, qkv_attn.hip; HOST_SIZED only): q, k, v are the
+// granules a.qkv_tag the same launch's GEMV workgroups publish. Wave 0 holds them: it first
+// polls one granule of the head's v row from one address (one line per poll, s_sleep between
+// -- 1,024 pollers beside the weight stream), then every granule it needs until all carry this
+// layer's tag; the K/V rows are in flight meanwhile.
+template <typename KT, typename IO, bool HOST_SIZED = false, bool TAGGED = false>
 __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, int ns, float* smem,
                                           const WgStamp* ts = nullptr) {
+    static_assert(!TAGGED || HOST_SIZED, "the fused launch sizes the attention grid on the host");
     float* q_s = smem;
     float* kcur_s = q_s + D;
     float* vcur_s = kcur_s + D;
@@ -185,6 +196,17 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     float pq0 = 0.f, pq1 = 0.f, pk0 = 0.f, pk1 = 0.f, pv = 0.f;
     long long psd = 0;
     int pos;
+    unsigned want = 0;  // TAGGED: this layer's tag
+    unsigned long long gq0 = 0, gq1 = 0, gk0 = 0, gk1 = 0, gv0 = 0, gv1 = 0;
+    const unsigned long long* qt = nullptr;
+    const unsigned long long* kt = nullptr;
+    const unsigned long long* vt = nullptr;
+    if constexpr (TAGGED) {
+        want = *a.tag_epoch * 128u + a.tag_layer;
+        qt = a.qkv_tag + (size_t)h * D;
+        kt = a.qkv_tag + (size_t)(a.heads + kvh) * D;
+        vt = a.qkv_tag + (size_t)(a.heads + a.kv_heads + kvh) * D;
+    }
     if constexpr (HOST_SIZED) {
         // the launcher requires a device position here. The load goes through a per-lane
         // (opaque zero) index so the compiler keeps it in a VGPR: as a uniform value it was
@@ -200,6 +222,13 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
             vr[t] = ld_raw(vc + (size_t)jj * D + l16 * 8);
         }
         const int i = tid & (D / 2 - 1);
+        if constexpr (TAGGED) {
+            if (tid < kWave) {  // wave 0's first look at its granules (almost never ready yet)
+                gq0 = ld_granule(qt + i); gq1 = ld_granule(qt + i + D / 2);
+                gk0 = ld_granule(kt + i); gk1 = ld_granule(kt + i + D / 2);
+                gv0 = ld_granule(vt + i); gv1 = ld_granule(vt + i + D / 2);
+            }
+        } else {
         pq0 = IO::ld(qrow + i);
         pq1 = IO::ld(qrow + i + D / 2);
         // the current k and v (used by the split owning the position; loaded by every
@@ -207,6 +236,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
         pk0 = IO::ld(krow + i);
         pk1 = IO::ld(krow + i + D / 2);
         pv = IO::ld(vrow + (tid & (D - 1)));
+        }
         if (a.xacc != nullptr && split == 0 && a.resid_fixed != nullptr)
             psd = a.resid_fixed[min(h * seed_per + tid, a.hidden - 1)];
     } else {
@@ -218,7 +248,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
         // the grid (and the o_proj's merge count) came from the host's position: if the
         // device state disagrees, keys past nact * CH would be dropped or stale partials
         // merged -- report it (tokens_out raises) instead of computing a wrong token
-        if (pos / CH + 1 != (int)gridDim.y) {
+        if (pos / CH + 1 != a.nact) {
             if (a.err != nullptr && tid == 0 && split == 0) atomicOr(a.err, 4);
             return;
         }
@@ -245,6 +275,41 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
 
     // ---- q (and the current k, v when this block owns position `pos`)
     const float qscale = 1.0f / sqrtf((float)D);
+    if constexpr (TAGGED) {
+        if (tid < kWave) {
+            auto rdy = [&](unsigned long long g) { return (unsigned)(g >> 32) == want; };
+            auto all6 = [&]() { return rdy(gq0) && rdy(gq1) && rdy(gk0) && rdy(gk1) && rdy(gv0) && rdy(gv1); };
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            bool dead = false;
+            if (!__all(all6())) {
+                // phase 1: one granule (the head's last v element), one line per poll
+                int z = 0;
+                asm volatile("" : "+v"(z));  // a per-lane address: never a scalar-cache load
+                while ((unsigned)(ld_granule(vt + (D - 1) + z) >> 32) != want) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) { dead = true; break; }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                // phase 2: every granule, re-loading the ones still stale
+                while (!dead && !__all(all6())) {
+                    if (!rdy(gq0)) gq0 = ld_granule(qt + tid);
+                    if (!rdy(gq1)) gq1 = ld_granule(qt + tid + D / 2);
+                    if (!rdy(gk0)) gk0 = ld_granule(kt + tid);
+                    if (!rdy(gk1)) gk1 = ld_granule(kt + tid + D / 2);
+                    if (!rdy(gv0)) gv0 = ld_granule(vt + tid);
+                    if (!rdy(gv1)) gv1 = ld_granule(vt + tid + D / 2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) dead = true;
+                }
+            }
+            if (dead && tid == 0 && a.err != nullptr) atomicOr(a.err, 64);
+            if (tid == 0) ml_s[2] = dead ? 1.f : 0.f;
+            pq0 = __uint_as_float((unsigned)gq0); pq1 = __uint_as_float((unsigned)gq1);
+            pk0 = __uint_as_float((unsigned)gk0); pk1 = __uint_as_float((unsigned)gk1);
+            if (owns_pos) {
+                vcur_s[tid] = cache_round<KT>(__uint_as_float((unsigned)gv0));
+                vcur_s[tid + D / 2] = cache_round<KT>(__uint_as_float((unsigned)gv1));
+            }
+        }
+    }
     if (tid < D / 2) {
         const int i = tid;
         float c = 1.f, s = 0.f;
@@ -264,10 +329,13 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
             kcur_s[i] = cache_round<KT>(k0 * c - k1 * s);
             kcur_s[i + D / 2] = cache_round<KT>(k1 * c + k0 * s);
         }
-    } else if (owns_pos && tid >= D && tid < 2 * D) {
+    } else if (!TAGGED && owns_pos && tid >= D && tid < 2 * D) {
         vcur_s[tid - D] = cache_round<KT>(HOST_SIZED ? pv : IO::ld(vrow + tid - D));
     }
     __syncthreads();
+    if constexpr (TAGGED) {
+        if (ml_s[2] != 0.f) return;  // rows never arrived (error bit 64): no partials
+    }
     if (ts) ts->mark(1);  // timeline: q rotated, this split's K/V rows in registers
 
     if (owns_pos && (h % group) == 0 && tid < D) {

@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -104,6 +105,9 @@ struct StepGraphs {
 #ifndef LLMI_SEED_FROM_DOWN
 #define LLMI_SEED_FROM_DOWN 1  // single rank: down seeds the next o_proj sum; the attention writes no seed (0: A/B)
 #endif
+#ifndef LLMI_QKV_ATTN
+#define LLMI_QKV_ATTN 0  // one q/k/v GEMV + attention launch (qkv_attn.hip); engine option "qkv_attn"
+#endif
 #ifndef LLMI_DOWN_STORE
 #define LLMI_DOWN_STORE 1  // unsplit down: rows written as xmid + fixed(y), not seeded + atomically added (0: A/B)
 #endif
@@ -151,6 +155,10 @@ struct Engine {
 
     StepGraphs graphs;
     int rec_nact = 0;  // active split count the next recorded step's attention is sized for
+    // fused q/k/v + attention launch (qkv_attn.hip) where the shapes allow it; option "qkv_attn",
+    // default LLMI_QKV_ATTN (A/B); qtag: its granule buffer [(heads + 2 kv) * d]
+    bool qa_fuse = LLMI_QKV_ATTN != 0;
+    unsigned long long* qtag = nullptr;
     ncclComm_t comm = nullptr;
     // one-shot peer exchange (xchg.hip): this rank's inbox (uncached HBM), every rank's
     // inbox base (IPC-mapped for peers) in device memory, per-slice epoch counters.
@@ -372,6 +380,7 @@ struct Engine {
         const size_t o_par = take((size_t)lm_grid * 8);
         const size_t o_pr = take((size_t)c.max_seq * 4), o_tok = take((size_t)(c.max_seq + 1) * 4);
         const size_t o_rope = take((size_t)c.max_seq * c.head_dim * 4);
+        const size_t o_qtag = take((size_t)(ql + 2 * kvrows) * 8);
             LLMI_HIP(hipMalloc(&scratch, off));
         LLMI_HIP(hipMemsetAsync(scratch, 0, off, stream));
         attn_ws = scratch + o_ws;
@@ -388,6 +397,7 @@ struct Engine {
         prompt = (int32_t*)(scratch + o_pr);
         tokens = (int32_t*)(scratch + o_tok);
         rope_tab = (float*)(scratch + o_rope);
+        qtag = (unsigned long long*)(scratch + o_qtag);  // zeroed: tag 0 never matches (epochs start at 1)
         // cos/sin cache with HF's fp32 arithmetic (LlamaRotaryEmbedding._set_cos_sin_cache):
         // inv_freq = 1 / fp32(base ** (2i/d)) (torch's fp32 pow is correctly rounded),
         // angle = fp32(pos * inv_freq), cos/sin correctly rounded to fp32
@@ -750,8 +760,18 @@ struct Engine {
                                  nullptr, 0, stream);
     }
     int rec_attn(int l) {
-        LLMI_TRY(gemv_launch(qkv_args(l), stream));
-        LLMI_TRY(attn_decode_launch(attn_args(l), stream));
+        GemvArgs q = qkv_args(l);
+        AttnArgs at = attn_args(l);
+        if (qa_fuse && qtag && l < 128) {
+            q.y_tag = qtag; q.tag_epoch = &st->epoch; q.tag_layer = (unsigned)l;
+            at.qkv_tag = qtag; at.tag_epoch = &st->epoch; at.tag_layer = (unsigned)l;
+        }
+        if (at.qkv_tag && qkv_attn_supported(q, at)) {  // one launch, q/k/v as tagged granules
+            LLMI_TRY(qkv_attn_launch(q, at, stream));
+        } else {
+            LLMI_TRY(gemv_launch(q, stream));
+            LLMI_TRY(attn_decode_launch(at, stream));
+        }
         OprojArgs o = o_args(l);
         if (tail_mode) {  // the o_proj launch pushes (and reduces) xacc itself
             o.xt = xchg_args(xacc, c.hidden, 0, tail_mode);
@@ -848,8 +868,11 @@ struct Engine {
         if (name == "kpar") {
             LLMI_REQUIRE(value == 0 || value == 1, "set_option kpar: 1 on (default), 0 off");
             kpar_off = value == 0;
+        } else if (name == "qkv_attn") {
+            LLMI_REQUIRE(value == 0 || value == 1, "set_option qkv_attn: 1 one q/k/v + attention launch, 0 two");
+            qa_fuse = value == 1;
         } else {
-            LLMI_REQUIRE(false, "set_option: unknown option (kpar)");
+            LLMI_REQUIRE(false, "set_option: unknown option (kpar, qkv_attn)");
         }
         graphs.clear();  // the captured steps change
         return LLMI_OK;
@@ -991,7 +1014,9 @@ struct Engine {
         h.vocab = c.vocab;
         h.error = 0;
         LLMI_HIP(hipMemcpyAsync(prompt, ids, (size_t)n * 4, hipMemcpyHostToDevice, stream));
-        LLMI_HIP(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, stream));
+        // (the epoch and what follows it are left alone: the fused q/k/v launch's granule tags
+        // must never repeat the tag its buffer already holds, across prompts too)
+        LLMI_HIP(hipMemcpyAsync(st, &h, offsetof(DecodeState, epoch), hipMemcpyHostToDevice, stream));
         LLMI_HIP(hipStreamSynchronize(stream));
         host_next_pos = 0;
         prompt_len = n;
@@ -1296,7 +1321,8 @@ struct Engine {
         LLMI_REQUIRE(h.error == 0, "decode: device error flag " + std::to_string(h.error) +
                                        " (1: token id out of range, 2: position overflow, 4: attention split count != device position, "
                                        "8: a tensor-parallel peer never arrived (one-shot exchange timeout), "
-                                       "16: a prefill gate_up lo partial never arrived, 32: a ring-layer hand-off timed out)");
+                                       "16: a prefill gate_up lo partial never arrived, 32: a ring-layer hand-off timed out, "
+                                       "64: a fused q/k/v + attention wait timed out)");
         const int m = n < valid ? n : valid;
         if (m > 0) LLMI_HIP(hipMemcpy(out, tokens, (size_t)m * 4, hipMemcpyDeviceToHost));
         if (n_valid) *n_valid = valid;

@@ -88,9 +88,14 @@ __host__ __device__ inline size_t gemv_lds_bytes(int k) {
 // XPT: float4s of x each thread holds in registers during staging (k <= XPT*4*256);
 // 0 = generic strided staging (standalone only).
 // bid / nblk: this workgroup's index in the GEMV grid and the grid size.
+// TAG (EPI_STORE only; the fused q/k/v + attention launch, qkv_attn.hip): rows go out as
+// write-through {fp32 bits, tag} granules in a.y_tag instead of fp32 stores in a.y.
 template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, typename IO,
-          int KPT = 1>
+          int KPT = 1, bool TAG = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, float4* xs) {
+    static_assert(!TAG || EPI == EPI_STORE, "granule rows: store epilogue only");
+    // the tag's epoch is one scalar load, issued first (consumed in the first epilogue)
+    const unsigned long long tag_hi = TAG ? (unsigned long long)(*a.tag_epoch * 128u + a.tag_layer) << 32 : 0ull;
     // residual hand-over (seed_dst <- seed_src slice)
     auto seed = [&, bid0 = bid, nblk0 = nblk]() {
         if (a.seed_dst == nullptr) return;
@@ -297,6 +302,9 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
                             atomicAdd(reinterpret_cast<unsigned long long*>(a.yacc + row),
                                       (unsigned long long)to_fixed(v));
                         }
+                    } else if constexpr (TAG) {
+                        __hip_atomic_store(a.y_tag + row, tag_hi | (unsigned long long)__float_as_uint(v),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } else {
                         if (EPI == EPI_ADD) v += a.resid_scale * IO::ld(a.resid + row);
                         IO::st(a.y + row, v);

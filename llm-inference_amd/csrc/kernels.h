@@ -84,6 +84,13 @@ struct GemvArgs {
     // adds them in order. Grid = ceil(groups / (4 / kpar)), every wave exactly one group.
     // EPI_STORE / EPI_SILU_MUL only; 0 / 1 = off.
     int kpar = 0;
+    // EPI_STORE inside the fused q/k/v + attention launch (qkv_attn.hip): row r is published as
+    // the 8-byte granule {fp32 bits, tag} in y_tag[r] (one write-through store), tag =
+    // *tag_epoch * 128 + tag_layer, so the attention workgroups of the same launch can tell a
+    // finished row from the previous layer's without any flag or fence
+    unsigned long long* y_tag = nullptr;
+    const unsigned* tag_epoch = nullptr;
+    unsigned tag_layer = 0;
 };
 
 
@@ -283,6 +290,12 @@ struct AttnArgs {
     // HOST_SIZED (nact > 0): the kernel checks nact against the device position; on a
     // mismatch it sets bit 4 here (DecodeState::error) and does no work
     int* err = nullptr;
+    // fused q/k/v + attention launch (qkv_attn.hip): q, k, v come from the GEMV's granules
+    // {fp32 bits, tag} of this launch (qkv_tag, polled until every tag is
+    // *tag_epoch * 128 + tag_layer) instead of qkv; a wait past ~2 s sets error bit 64
+    const unsigned long long* qkv_tag = nullptr;
+    const unsigned* tag_epoch = nullptr;
+    unsigned tag_layer = 0;
 };
 
 // Merge of the split partials fused into the o_proj, split by head: workgroup
@@ -360,6 +373,10 @@ __host__ __device__ __forceinline__ float from_fixed(long long v) {
 constexpr int kAttnChunk = LLMI_ATTN_CH;  // cached positions per workgroup (split-KV)
 size_t attn_workspace_bytes(int heads, int head_dim, int max_seq);
 int attn_decode_launch(const AttnArgs& a, hipStream_t s);
+// the q/k/v GEMV (g: EPI_STORE, rmsnorm, fixed-point x) and the attention (at: host-sized)
+// of one decode layer as ONE launch, q/k/v handed over as tagged granules (qkv_attn.hip)
+bool qkv_attn_supported(const GemvArgs& g, const AttnArgs& at);
+int qkv_attn_launch(const GemvArgs& g, const AttnArgs& at, hipStream_t s);
 
 // ------------------------------------------------------ decode-loop state
 struct DecodeState {
@@ -371,8 +388,11 @@ struct DecodeState {
                       // 4: host-sized attention grid != device position's split count,
                       // 8: a tensor-parallel peer never arrived (one-shot exchange timeout, xchg.hip),
                       // 16: a prefill gate_up lo partial never arrived, gemm3_silu_bal_kernel,
-                      // 32: a ring-layer hand-off or ring-slot wait timed out, ring.hip)
-    int pad[3];
+                      // 32: a ring-layer hand-off or ring-slot wait timed out, ring.hip,
+                      // 64: a fused q/k/v + attention workgroup's wait for its rows timed out)
+    unsigned epoch;   // forwards stepped since the engine was created (step_start; never reset
+                      // by set_prompt): tags the fused q/k/v launch's granules
+    int pad[2];
 };
 
 // step start: pick the token for position next_pos (prompt id or argmax of

@@ -176,7 +176,10 @@ __global__ void step_start_kernel(DecodeState* st, const int32_t* prompt, const 
     __shared__ int tok_s;
     const int p = st->next_pos;
     if (p >= max_seq) {  // host guards this; keep the state consistent if it does not
-        if (threadIdx.x == 0) atomicOr(&st->error, 2);
+        if (threadIdx.x == 0) {
+            atomicOr(&st->error, 2);
+            st->epoch = st->epoch + 1u;
+        }
         return;
     }
     int tok;
@@ -201,6 +204,7 @@ __global__ void step_start_kernel(DecodeState* st, const int32_t* prompt, const 
         tokens[p] = tok;
         st->cur_pos = p;
         st->next_pos = p + 1;
+        st->epoch = st->epoch + 1u;  // tags this forward's fused q/k/v granules (qkv_attn.hip)
     }
     const TT* row = table + (size_t)tok * hidden;
     for (int i = threadIdx.x; i < hidden; i += blockDim.x) {
