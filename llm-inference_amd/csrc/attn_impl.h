@@ -285,7 +285,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
                 // phase 1: one granule (the head's last v element), one line per poll
                 int z = 0;
                 asm volatile("" : "+v"(z));  // a per-lane address: never a scalar-cache load
-                while ((unsigned)(ld_granule(vt + (D - 1) + z) >> 32) != want) {
+                while (!a.tag_poll_all && (unsigned)(ld_granule(vt + (D - 1) + z) >> 32) != want) {
                     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) { dead = true; break; }
                     __builtin_amdgcn_s_sleep(8);
                 }
@@ -298,6 +298,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
                     if (!rdy(gv0)) gv0 = ld_granule(vt + tid);
                     if (!rdy(gv1)) gv1 = ld_granule(vt + tid + D / 2);
                     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) dead = true;
+                    if (a.tag_poll_all) __builtin_amdgcn_s_sleep(4);
                 }
             }
             if (dead && tid == 0 && a.err != nullptr) atomicOr(a.err, 64);

@@ -871,8 +871,15 @@ struct Engine {
         } else if (name == "qkv_attn") {
             LLMI_REQUIRE(value == 0 || value == 1, "set_option qkv_attn: 1 one q/k/v + attention launch, 0 two");
             qa_fuse = value == 1;
+        } else if (name == "qa_grid") {
+            LLMI_REQUIRE(value >= 0, "set_option qa_grid: workgroups of the fused launch's GEMV part (0 = all resident)");
+            qkv_attn_set_grid(value);
+        } else if (name == "qa_order") {
+            qkv_attn_set_order(value);
+        } else if (name == "qa_poll") {
+            qkv_attn_set_poll(value);
         } else {
-            LLMI_REQUIRE(false, "set_option: unknown option (kpar, qkv_attn)");
+            LLMI_REQUIRE(false, "set_option: unknown option (kpar, qkv_attn, qa_grid, qa_order, qa_poll)");
         }
         graphs.clear();  // the captured steps change
         return LLMI_OK;

@@ -137,6 +137,15 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, int bid, int nblk, 
     const float4* x4 = reinterpret_cast<const float4*>(a.x + (size_t)ks * k);
 
     auto rows_of = [&](int g, int* rows) {
+        if constexpr (TAG) {
+            // head-major order (a.tag_heads > 0, MHA): group g of head h's q, k, v rows in turn,
+            // so a head's rows finish together and its attention can start while later heads'
+            // rows stream (64 two-row groups per 128-row head block)
+            if (a.tag_heads > 0) {
+                const int h = g / 192, rem = g - 192 * h, t = rem >> 6;
+                g = t * a.tag_heads * 64 + h * 64 + (rem & 63);
+            }
+        }
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) rows[r] = (EPI == EPI_SILU_MUL) ? g + r * a.pair_off : g * ROWS + r;
     };

@@ -91,6 +91,7 @@ struct GemvArgs {
     unsigned long long* y_tag = nullptr;
     const unsigned* tag_epoch = nullptr;
     unsigned tag_layer = 0;
+    int tag_heads = 0;  // > 0 (= heads = kv_heads, head_dim 128): rows computed head-major (q, k, v of head 0 first)
 };
 
 
@@ -296,6 +297,7 @@ struct AttnArgs {
     const unsigned long long* qkv_tag = nullptr;
     const unsigned* tag_epoch = nullptr;
     unsigned tag_layer = 0;
+    int tag_poll_all = 0;  // 1: poll every granule from the first look (no single-granule phase)
 };
 
 // Merge of the split partials fused into the o_proj, split by head: workgroup
@@ -377,6 +379,9 @@ int attn_decode_launch(const AttnArgs& a, hipStream_t s);
 // of one decode layer as ONE launch, q/k/v handed over as tagged granules (qkv_attn.hip)
 bool qkv_attn_supported(const GemvArgs& g, const AttnArgs& at);
 int qkv_attn_launch(const GemvArgs& g, const AttnArgs& at, hipStream_t s);
+void qkv_attn_set_grid(int cap);  // A/B: cap the GEMV part of the fused grid (0: all resident slots)
+void qkv_attn_set_order(int head_major);  // A/B: 1 head-major rows + attention blocks (default), 0 natural
+void qkv_attn_set_poll(int all);          // A/B: 1 poll every granule from the start, 0 one granule first (default)
 
 // ------------------------------------------------------ decode-loop state
 struct DecodeState {

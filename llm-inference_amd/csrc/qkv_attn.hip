@@ -22,8 +22,6 @@
 //
 // Results are bitwise those of the two launches: the GEMV and attention bodies are the same
 // code (gemv_body with TAG, attn_body with TAGGED), only the q/k/v transport differs.
-#include <cstdlib>
-
 #include "attn_impl.h"
 #include "gemv_launch.h"
 
@@ -35,6 +33,10 @@ template <typename WT, int U> constexpr int qa_minw() { return (sizeof(WT) >= 2 
 namespace llmi {
 namespace {
 
+int qa_grid_cap = 0;  // A/B: cap on the GEMV part of the grid (0 = every resident slot); qkv_attn_set_grid
+int qa_order = 1;     // 1: GEMV rows and attention blocks head-major (MHA); 0: natural order (A/B)
+int qa_poll_all = 0;  // 1: attention polls every granule from the start (A/B)
+
 template <typename WT, typename GT, int XPT, int U, typename KT>
 __global__ __launch_bounds__(256, (qa_minw<WT, U>())) void qkv_attn_kernel(GemvArgs g, AttnArgs at, int g_grid, int ns) {
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
@@ -43,9 +45,12 @@ __global__ __launch_bounds__(256, (qa_minw<WT, U>())) void qkv_attn_kernel(GemvA
         gemv_detail::gemv_body<WT, gemv_detail::kRows, EPI_STORE, true, GT, XPT, U, true, PlainIO, 1, true>(
             g, blockIdx.x, g_grid, xs);
     } else {
+        // head-major block order with head-major rows (g.tag_heads): a head's splits dispatch
+        // together, in the order the GEMV finishes the heads
         const int b = (int)blockIdx.x - g_grid;
-        attn_detail::attn_body<KT, PlainIO, true, true>(at, b % at.heads, b / at.heads, ns,
-                                                        reinterpret_cast<float*>(xs));
+        const int h = g.tag_heads > 0 ? b / at.nact : b % at.heads;
+        const int sp = g.tag_heads > 0 ? b - h * at.nact : b / at.heads;
+        attn_detail::attn_body<KT, PlainIO, true, true>(at, h, sp, ns, reinterpret_cast<float*>(xs), &ts);
     }
 }
 
@@ -55,7 +60,7 @@ int launch_k(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
     const size_t lds = std::max(gemv_detail::gemv_lds_bytes(g.k), attn_detail::kAttnLds);
     int G = gemv_grid(g);
     // resident blocks of this kernel: the GEMV takes at most all of them (a looping grid), the
-    // attention blocks fill the slots GEMV blocks leave (LLMI_QA_GRID: GEMV grid for A/B)
+    // attention blocks fill the slots GEMV blocks leave
     static size_t occ_lds = ~(size_t)0;
     static int occ_blocks = 0;
     if (lds != occ_lds) {
@@ -66,13 +71,14 @@ int launch_k(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
         occ_lds = lds;
     }
     if (occ_blocks > 0 && G > occ_blocks) G = occ_blocks;
-    if (const char* e = std::getenv("LLMI_QA_GRID")) {
-        const int v = std::atoi(e);
-        if (v > 0 && v < G) G = v;
-    }
+    if (qa_grid_cap > 0 && qa_grid_cap < G) G = qa_grid_cap;
     const int ns = (at.max_seq + attn_detail::CH - 1) / attn_detail::CH;
     const int grid = G + at.heads * at.nact;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, g, at, G, ns);
+    GemvArgs gg = g;
+    AttnArgs aa = at;
+    gg.tag_heads = (qa_order && at.heads == at.kv_heads && g.n_rows == 3 * at.heads * attn_detail::D) ? at.heads : 0;
+    aa.tag_poll_all = qa_poll_all;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, gg, aa, G, ns);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }
@@ -118,6 +124,10 @@ bool qkv_attn_supported(const GemvArgs& g, const AttnArgs& at) {
     if (at.heads <= 0 || at.kv_heads <= 0 || at.heads % at.kv_heads != 0) return false;
     return g.n_rows == (at.heads + 2 * at.kv_heads) * attn_detail::D;
 }
+
+void qkv_attn_set_grid(int cap) { qa_grid_cap = cap > 0 ? cap : 0; }
+void qkv_attn_set_order(int head_major) { qa_order = head_major != 0; }
+void qkv_attn_set_poll(int all) { qa_poll_all = all != 0; }
 
 int qkv_attn_launch(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
     LLMI_REQUIRE(qkv_attn_supported(g, at), "qkv_attn: unsupported shape (qkv_attn_supported)");

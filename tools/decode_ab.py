@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--max-seq", type=int, default=2048)
     ap.add_argument("--preset", default="llama2-7b")
     ap.add_argument("--int8", action="store_true")
+    ap.add_argument("--fixed", default="", help="options set once for every variant: name=value[,name=value]")
     a = ap.parse_args()
     cfg = preset(a.preset, layers=a.layers, max_seq=a.max_seq, tp_rank=0, tp_world=a.tp_world)
     cfg.kv_dtype = llmi.F16
@@ -40,6 +41,9 @@ def main():
     prompt = synth_prompt(0, 8, cfg.vocab)
     with Engine(cfg) as e:
         e.load_synthetic(0)
+        for kv in filter(None, a.fixed.split(",")):
+            k, v = kv.split("=")
+            e.set_option(k, int(v))
         if a.tp_world > 1:
             e.xchg_loopback()
             e.set_exchange(a.exchange)

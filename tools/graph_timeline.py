@@ -30,12 +30,17 @@ def wg_detail(host, stride, layer):
     round-robin dispatch) and the hardware CU id, for layer `layer`'s q/k/v, o and down, plus
     per-XCD completion quantiles: where a launch's tail comes from."""
     out = {}
-    for k, off in (("qkv", 0), ("attn", 1), ("o", 2), ("down", 4)):
+    for k, off in (("qkv", 0), ("attn", 1), ("o", 2), ("down", 4), ("qkv_attn_part", 0)):
         s = 5 * layer + off
         rows = host[s * stride:(s + 1) * stride].astype(np.int64)
-        idx = np.nonzero(rows[:, 0] > 0)[0]
+        sel = rows[:, 0] > 0
+        if off == 0:  # the fused q/k/v + attention launch: its attention blocks set mark 1
+            sel &= (rows[:, 1] > 0) if k == "qkv_attn_part" else (rows[:, 1] == 0)
+        idx = np.nonzero(sel)[0]
+        if not len(idx):
+            continue
         v = rows[idx]
-        t0 = v[:, 0].min()
+        t0 = rows[rows[:, 0] > 0][:, 0].min()  # the launch's first start (fused: either part)
         start, end = (v[:, 0] - t0) / 100.0, (v[:, 3] - t0) / 100.0
         xcd = idx % 8
         per_xcd = {}
@@ -69,6 +74,7 @@ def main():
     ap.add_argument("--wg-layer", type=int, default=-1,
                     help="also dump layer L's per-workgroup {start, end, xcd, cu} for q/k/v, o and down, "
                          "with completion quantiles per XCD (VERDICT r04 item 3a)")
+    ap.add_argument("--set", default="", help="engine options name=value[,name=value] (llmi_engine_set_option)")
     a = ap.parse_args()
     lib = _lib.lib()
     cfg = preset(a.preset, layers=a.layers, max_seq=2048, tp_rank=0, tp_world=a.tp_world)
@@ -82,6 +88,9 @@ def main():
            "mode": "hipGraph replay (one captured graph per active split count)", "ctx": {}}
     with Engine(cfg) as e:
         e.load_synthetic(0)
+        for kv in filter(None, a.set.split(",")):
+            k, v = kv.split("=")
+            e.set_option(k, int(v))
         if a.tp_world > 1:
             e.xchg_loopback()
             e.set_exchange(a.exchange)
