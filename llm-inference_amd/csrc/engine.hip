@@ -106,7 +106,7 @@ struct StepGraphs {
 #define LLMI_SEED_FROM_DOWN 1  // single rank: down seeds the next o_proj sum; the attention writes no seed (0: A/B)
 #endif
 #ifndef LLMI_QKV_ATTN
-#define LLMI_QKV_ATTN 0  // one q/k/v GEMV + attention launch (qkv_attn.hip); engine option "qkv_attn"
+#define LLMI_QKV_ATTN 1  // one q/k/v GEMV + attention launch (qkv_attn.hip); engine option "qkv_attn"
 #endif
 #ifndef LLMI_DOWN_STORE
 #define LLMI_DOWN_STORE 1  // unsplit down: rows written as xmid + fixed(y), not seeded + atomically added (0: A/B)
@@ -763,15 +763,19 @@ struct Engine {
         GemvArgs q = qkv_args(l);
         AttnArgs at = attn_args(l);
         if (qa_fuse && qtag && l < 128) {
-            q.y_tag = qtag; q.tag_epoch = &st->epoch; q.tag_layer = (unsigned)l;
-            at.qkv_tag = qtag; at.tag_epoch = &st->epoch; at.tag_layer = (unsigned)l;
+            GemvArgs qf = q;
+            qf.kpar = 0;  // the fused GEMV part streams a row group per wave (kpar: +0.3 % alone at TP 8)
+            qf.y_tag = qtag; qf.tag_epoch = &st->epoch; qf.tag_layer = (unsigned)l;
+            AttnArgs af = at;
+            af.qkv_tag = qtag; af.tag_epoch = &st->epoch; af.tag_layer = (unsigned)l;
+            if (qkv_attn_supported(qf, af)) return rec_oproj(l, qkv_attn_launch(qf, af, stream));  // one launch
         }
-        if (at.qkv_tag && qkv_attn_supported(q, at)) {  // one launch, q/k/v as tagged granules
-            LLMI_TRY(qkv_attn_launch(q, at, stream));
-        } else {
-            LLMI_TRY(gemv_launch(q, stream));
-            LLMI_TRY(attn_decode_launch(at, stream));
-        }
+        LLMI_TRY(gemv_launch(q, stream));
+        LLMI_TRY(attn_decode_launch(at, stream));
+        return rec_oproj(l, LLMI_OK);
+    }
+    int rec_oproj(int l, int prev) {
+        LLMI_TRY(prev);
         OprojArgs o = o_args(l);
         if (tail_mode) {  // the o_proj launch pushes (and reduces) xacc itself
             o.xt = xchg_args(xacc, c.hidden, 0, tail_mode);

@@ -95,9 +95,16 @@ int launch_w(const GemvArgs& g, const AttnArgs& at, int xpt, int u, hipStream_t 
     return u == 4 ? launch_kt<WT, GT, 5, 4>(g, at, s) : launch_kt<WT, GT, 5, 5>(g, at, s);
 }
 
+
 int epl_of(int dt) { return dt == LLMI_F16 ? 8 : dt == LLMI_F32 ? 4 : dt == LLMI_I8 ? 16 : 0; }
 
+// the GEMV part's unroll: 4 or 5 whenever that covers a row in whole batches (a TP rank's
+// few row groups would otherwise pick 8, which this kernel does not instantiate), else the
+// standalone GEMV's choice
 int pick_u(const GemvArgs& g) {
+    const int nc = g.k / epl_of(g.w_dtype);
+    if (nc % (64 * 4) == 0) return 4;
+    if (nc % (64 * 5) == 0) return 5;
     const int groups = (g.n_rows + gemv_detail::kRows - 1) / gemv_detail::kRows;
     switch (g.w_dtype) {
         case LLMI_F16: return gemv_detail::pick_unroll<__half, EPI_STORE>(g, groups);
