@@ -243,18 +243,31 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
         pos = a.pos_dev ? *a.pos_dev : a.pos_host;
     }
 
-    if (pos < 0 || pos >= a.max_seq) return;  // host validates; guard against a stale state
+    // an error exit still arrives on the head's counter (publish), so the fused o_proj blocks
+    // never wait out their bound behind a workgroup that reported an error already
+    auto arrive_on_error = [&]() {
+        if (a.publish && tid == 0)
+            atomicAdd(ws_carve(a.workspace, a.heads, ns).counters + (size_t)h * kCntWordsPerHead, 1u);
+    };
+    if (pos < 0 || pos >= a.max_seq) {  // host validates; guard against a stale state
+        arrive_on_error();
+        return;
+    }
     if constexpr (HOST_SIZED) {
         // the grid (and the o_proj's merge count) came from the host's position: if the
         // device state disagrees, keys past nact * CH would be dropped or stale partials
         // merged -- report it (tokens_out raises) instead of computing a wrong token
         if (pos / CH + 1 != a.nact) {
             if (a.err != nullptr && tid == 0 && split == 0) atomicOr(a.err, 4);
+            arrive_on_error();
             return;
         }
     }
     const int ctx = pos + 1;
-    if (start >= ctx) return;
+    if (start >= ctx) {
+        arrive_on_error();
+        return;
+    }
     const int end = min(start + CH, ctx);
     const int nact = (ctx + CH - 1) / CH;
     const bool owns_pos = (end == ctx);
@@ -335,7 +348,10 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     }
     __syncthreads();
     if constexpr (TAGGED) {
-        if (ml_s[2] != 0.f) return;  // rows never arrived (error bit 64): no partials
+        if (ml_s[2] != 0.f) {  // rows never arrived (error bit 64): no partials
+            arrive_on_error();
+            return;
+        }
     }
     if (ts) ts->mark(1);  // timeline: q rotated, this split's K/V rows in registers
 
@@ -416,6 +432,23 @@ __device__ __forceinline__ void attn_body(const AttnArgs& a, int h, int split, i
     }
     if (ts) ts->mark(2);  // timeline: scores, softmax and P V done
     Ws ws = ws_carve(a.workspace, a.heads, ns);
+    if (a.publish) {
+        // the o_proj blocks of the same launch read these: every store write-through (sc1), each
+        // storing wave drained, then ONE arrival per workgroup (microarch guide, hand-off table row 1)
+        auto st_wt = [](float* p, float v) {
+            __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        };
+        if (tid < D) st_wt(ws.o + ((size_t)h * ns + split) * D + tid, o);
+        if (tid == 0) {
+            st_wt(ws.ml + ((size_t)h * ns + split) * 2 + 0, ml_s[0]);
+            st_wt(ws.ml + ((size_t)h * ns + split) * 2 + 1, ml_s[1]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) atomicAdd(ws.counters + (size_t)h * kCntWordsPerHead, 1u);
+        return;  // (no residual seed: the fused launch runs only where xacc is seeded before it)
+    }
     if (tid < D) IO::st(ws.o + ((size_t)h * ns + split) * D + tid, o);
     if (tid == 0) {
         IO::st(ws.ml + ((size_t)h * ns + split) * 2 + 0, ml_s[0]);
@@ -610,7 +643,18 @@ __device__ __forceinline__ void oproj_body(const OprojArgs& a, int h, int chunk,
 template <int NPL>
 constexpr size_t oproj2_lds() { return (4 * kMaxSplits + 4 + 2 * D + 2 * 8 * NPL) * sizeof(float); }
 
-template <typename WT, int NPL, typename IO>
+// FUSED (the o_proj part of the fused q/k/v + attention + o_proj launch, qkv_attn.hip): the W_o
+// slices are issued first (they do not depend on this token), then one lane polls the two heads'
+// arrival counters until all a.nact splits have published, and every partial is read with sc1
+// loads after the workgroup barrier; the pair's last departing workgroup re-zeroes the counters
+// for the next launch (counters word 0 of head 2 hp and 2 hp + 1: arrivals; word 1 of head 2 hp:
+// departures).
+__device__ __forceinline__ float ld_wt(const float* p) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <typename WT, int NPL, typename IO, bool FUSED = false>
 __device__ __forceinline__ void oproj_body2(const OprojArgs& a, int hp, int chunk, int ns, float* smem) {
     float* m_s = smem;                      // [2][kMaxSplits]
     float* l_s = m_s + 2 * kMaxSplits;      // [2][kMaxSplits]
@@ -631,34 +675,57 @@ __device__ __forceinline__ void oproj_body2(const OprojArgs& a, int hp, int chun
     constexpr int kOv = 2 * kMergeChunk;
     float ov[kOv];
     const int nl = a.nact > 0 ? min(a.nact, ns) : ns;
-    // issue order as oproj_body: partials, (m, l), then the W_o slices, before any wait
-#pragma unroll
-    for (int i = 0; i < kOv; ++i) ov[i] = IO::ld(oh + (size_t)(i < nl ? i : 0) * D);
     constexpr int kMlPer = kMaxSplits / (kThreads / 2);
     float mr[kMlPer], lr[kMlPer];
+    W8<WT> wr[NPL];
+    auto load_w = [&]() {
+#pragma unroll
+        for (int t = 0; t < NPL; ++t) {
+            int row = row0 + g8 + 8 * t;
+            row = row < a.n_rows ? row : a.n_rows - 1;
+            if constexpr (sizeof(WT) == 1 && NPL >= 2) {
+                if (t < NPL / 2) {  // int8: two rows per 16-lane group, 8 lanes each (as oproj_load_w)
+                    int r2 = row0 + g8 + 8 * (2 * t + (l16 >> 3));
+                    r2 = r2 < a.n_rows ? r2 : a.n_rows - 1;
+                    wr[t].v[0] = ld_nt16(w + (size_t)r2 * a.ldw + (size_t)h * D + (l16 & 7) * 16);
+                }
+            } else {
+                wr[t] = ld_w8<WT>(w + (size_t)row * a.ldw + (size_t)h * D + l16 * 8);
+            }
+        }
+    };
+    auto ld_p = [&](const float* p) { return FUSED ? ld_wt(p) : IO::ld(p); };
+    if constexpr (FUSED) {
+        load_w();
+        unsigned* arr0 = ws.counters + (size_t)(2 * hp) * kCntWordsPerHead;
+        unsigned* arr1 = arr0 + kCntWordsPerHead;
+        if (tid == 0) {
+            const unsigned want = (unsigned)nl;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            bool dead = false;
+            while (__hip_atomic_load(arr0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want ||
+                   __hip_atomic_load(arr1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) { dead = true; break; }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (dead && a.err) atomicOr(a.err, 64);
+            linv_s[2] = dead ? 1.f : 0.f;
+        }
+        __syncthreads();
+        if (linv_s[2] != 0.f) return;
+    }
+    // issue order as oproj_body: partials, (m, l), then the W_o slices, before any wait
+#pragma unroll
+    for (int i = 0; i < kOv; ++i) ov[i] = ld_p(oh + (size_t)(i < nl ? i : 0) * D);
 #pragma unroll
     for (int i = 0; i < kMlPer; ++i) {
         if (i * (kThreads / 2) < nl) {
             const int sp = min(d + i * (kThreads / 2), nl - 1);
-            mr[i] = IO::ld(mlh + 2 * sp);
-            lr[i] = IO::ld(mlh + 2 * sp + 1);
+            mr[i] = ld_p(mlh + 2 * sp);
+            lr[i] = ld_p(mlh + 2 * sp + 1);
         }
     }
-    W8<WT> wr[NPL];
-#pragma unroll
-    for (int t = 0; t < NPL; ++t) {
-        int row = row0 + g8 + 8 * t;
-        row = row < a.n_rows ? row : a.n_rows - 1;
-        if constexpr (sizeof(WT) == 1 && NPL >= 2) {
-            if (t < NPL / 2) {  // int8: two rows per 16-lane group, 8 lanes each (as oproj_load_w)
-                int r2 = row0 + g8 + 8 * (2 * t + (l16 >> 3));
-                r2 = r2 < a.n_rows ? r2 : a.n_rows - 1;
-                wr[t].v[0] = ld_nt16(w + (size_t)r2 * a.ldw + (size_t)h * D + (l16 & 7) * 16);
-            }
-        } else {
-            wr[t] = ld_w8<WT>(w + (size_t)row * a.ldw + (size_t)h * D + l16 * 8);
-        }
-    }
+    if constexpr (!FUSED) load_w();
 #pragma unroll
     for (int i = 0; i < kMlPer; ++i) {
         const int sp = d + i * (kThreads / 2);
@@ -704,12 +771,25 @@ __device__ __forceinline__ void oproj_body2(const OprojArgs& a, int hp, int chun
             O1 = fmaf(s1 < nact ? ov[s1] : 0.f, s1 < nact ? mw[s1] : 0.f, O1);
         }
         for (int sp = kOv; sp < nact; sp += 2) {
-            O0 = fmaf(IO::ld(oh + (size_t)sp * D), mw[sp], O0);
-            if (sp + 1 < nact) O1 = fmaf(IO::ld(oh + (size_t)(sp + 1) * D), mw[sp + 1], O1);
+            O0 = fmaf(ld_p(oh + (size_t)sp * D), mw[sp], O0);
+            if (sp + 1 < nact) O1 = fmaf(ld_p(oh + (size_t)(sp + 1) * D), mw[sp + 1], O1);
         }
         o_s[mh * D + d] = (O0 + O1) * linv_s[mh];
     }
     __syncthreads();
+    if constexpr (FUSED) {
+        // every partial of this workgroup is read (the barrier above): depart; the pair's last
+        // workgroup re-zeroes both arrival counters and the departure counter
+        if (tid == 0) {
+            unsigned* arr0 = ws.counters + (size_t)(2 * hp) * kCntWordsPerHead;
+            const int n_chunks = (a.n_rows + 8 * NPL - 1) / (8 * NPL);
+            if (atomicAdd(arr0 + 1, 1u) == (unsigned)(n_chunks - 1)) {
+                __hip_atomic_store(arr0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(arr0 + kCntWordsPerHead, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(arr0 + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
     float* yh = y_s + hs * 8 * NPL;
     const float* oh_s = o_s + hs * D;
     if constexpr (sizeof(WT) == 1 && NPL >= 2) {

@@ -108,6 +108,9 @@ struct StepGraphs {
 #ifndef LLMI_QKV_ATTN
 #define LLMI_QKV_ATTN 1  // one q/k/v GEMV + attention launch (qkv_attn.hip); engine option "qkv_attn"
 #endif
+#ifndef LLMI_QKV_ATTN_O
+#define LLMI_QKV_ATTN_O 0  // the fused launch also runs the o_proj (fp16 MHA, single rank); option "qa_o"
+#endif
 #ifndef LLMI_DOWN_STORE
 #define LLMI_DOWN_STORE 1  // unsplit down: rows written as xmid + fixed(y), not seeded + atomically added (0: A/B)
 #endif
@@ -158,6 +161,7 @@ struct Engine {
     // fused q/k/v + attention launch (qkv_attn.hip) where the shapes allow it; option "qkv_attn",
     // default LLMI_QKV_ATTN (A/B); qtag: its granule buffer [(heads + 2 kv) * d]
     bool qa_fuse = LLMI_QKV_ATTN != 0;
+    bool qa_o = LLMI_QKV_ATTN_O != 0;  // ... with the o_proj in the same launch (option "qa_o")
     unsigned long long* qtag = nullptr;
     ncclComm_t comm = nullptr;
     // one-shot peer exchange (xchg.hip): this rank's inbox (uncached HBM), every rank's
@@ -683,7 +687,7 @@ struct Engine {
         a.out = attn_out; a.workspace = attn_ws;
         a.nact = rec_nact;
         a.err = &st->error;
-        if (l > 0 && seed_from_down()) a.xacc = nullptr;  // layer l - 1's down seeded xacc already
+        if (seed_from_down()) a.xacc = nullptr;  // layer l - 1's down (layer 0: step_start) seeded xacc already
         return a;
     }
     OprojArgs o_args(int l) const {
@@ -697,6 +701,7 @@ struct Engine {
         a.pos_dev = &st->cur_pos;
         a.workspace = attn_ws; a.xacc = xacc;
         a.nact = rec_nact;
+        a.err = &st->error;
         return a;
     }
     GemvArgs gu_args(int l) const {
@@ -757,7 +762,7 @@ struct Engine {
     // group (struct Group) can interleave its ranks between the reductions.
     int rec_start() {
         return step_start_launch(st, prompt, partials, lm_grid, tokens, embed, edt, c.hidden, x, res[0], c.max_seq,
-                                 nullptr, 0, stream);
+                                 nullptr, 0, stream, seed_from_down() ? xacc : nullptr);
     }
     int rec_attn(int l) {
         GemvArgs q = qkv_args(l);
@@ -768,15 +773,19 @@ struct Engine {
             qf.y_tag = qtag; qf.tag_epoch = &st->epoch; qf.tag_layer = (unsigned)l;
             AttnArgs af = at;
             af.qkv_tag = qtag; af.tag_epoch = &st->epoch; af.tag_layer = (unsigned)l;
-            if (qkv_attn_supported(qf, af)) return rec_oproj(l, qkv_attn_launch(qf, af, stream));  // one launch
+            OprojArgs o = o_args(l);
+            if (qa_o && !tail_mode && qkv_attn_o_supported(qf, af, o))  // q/k/v, attention and o_proj: one launch
+                return qkv_attn_o_launch(qf, af, &o, stream);
+            if (qkv_attn_supported(qf, af)) return rec_oproj(qkv_attn_launch(qf, af, stream), o);  // one launch
+            return rec_oproj(gemv_launch(q, stream), o, &at);
         }
         LLMI_TRY(gemv_launch(q, stream));
-        LLMI_TRY(attn_decode_launch(at, stream));
-        return rec_oproj(l, LLMI_OK);
+        return rec_oproj(LLMI_OK, o_args(l), &at);
     }
-    int rec_oproj(int l, int prev) {
+    // the layer's o_proj launch (after the attention launch when `at` is given)
+    int rec_oproj(int prev, OprojArgs o, const AttnArgs* at = nullptr) {
         LLMI_TRY(prev);
-        OprojArgs o = o_args(l);
+        if (at) LLMI_TRY(attn_decode_launch(*at, stream));
         if (tail_mode) {  // the o_proj launch pushes (and reduces) xacc itself
             o.xt = xchg_args(xacc, c.hidden, 0, tail_mode);
             o.xt_cnt = xt_cnt;
@@ -878,12 +887,14 @@ struct Engine {
         } else if (name == "qa_grid") {
             LLMI_REQUIRE(value >= 0, "set_option qa_grid: workgroups of the fused launch's GEMV part (0 = all resident)");
             qkv_attn_set_grid(value);
+        } else if (name == "qa_o") {
+            qa_o = value != 0;
         } else if (name == "qa_order") {
             qkv_attn_set_order(value);
         } else if (name == "qa_poll") {
             qkv_attn_set_poll(value);
         } else {
-            LLMI_REQUIRE(false, "set_option: unknown option (kpar, qkv_attn, qa_grid, qa_order, qa_poll)");
+            LLMI_REQUIRE(false, "set_option: unknown option (kpar, qkv_attn, qa_o, qa_grid, qa_order, qa_poll)");
         }
         graphs.clear();  // the captured steps change
         return LLMI_OK;

@@ -298,6 +298,9 @@ struct AttnArgs {
     const unsigned* tag_epoch = nullptr;
     unsigned tag_layer = 0;
     int tag_poll_all = 0;  // 1: poll every granule from the first look (no single-granule phase)
+    // 1 (the fused launch with its o_proj part): partials stored write-through, then one arrival
+    // per workgroup on the head's counter (workspace counters word 0) for the o_proj blocks
+    int publish = 0;
 };
 
 // Merge of the split partials fused into the o_proj, split by head: workgroup
@@ -320,6 +323,7 @@ struct OprojArgs {
     int nact = 0;  // > 0: active split count known on the host (no position read); see AttnArgs
     XchgArgs xt;              // producer-fused TP exchange of xacc (xt.buf null = off)
     unsigned* xt_cnt = nullptr;
+    int* err = nullptr;       // the fused launch's o_proj part: bit 64 when its heads never arrive
 };
 int attn_oproj_launch(const OprojArgs& a, hipStream_t s);
 
@@ -379,6 +383,10 @@ int attn_decode_launch(const AttnArgs& a, hipStream_t s);
 // of one decode layer as ONE launch, q/k/v handed over as tagged granules (qkv_attn.hip)
 bool qkv_attn_supported(const GemvArgs& g, const AttnArgs& at);
 int qkv_attn_launch(const GemvArgs& g, const AttnArgs& at, hipStream_t s);
+// ... and the layer's o_proj in the same launch (o non-null: fp16 weights, MHA, xacc seeded before
+// the launch -- the attention part seeds nothing -- and no fused exchange)
+bool qkv_attn_o_supported(const GemvArgs& g, const AttnArgs& at, const OprojArgs& o);
+int qkv_attn_o_launch(const GemvArgs& g, const AttnArgs& at, const OprojArgs* o, hipStream_t s);
 void qkv_attn_set_grid(int cap);  // A/B: cap the GEMV part of the fused grid (0: all resident slots)
 void qkv_attn_set_order(int head_major);  // A/B: 1 head-major rows + attention blocks (default), 0 natural
 void qkv_attn_set_poll(int all);          // A/B: 1 poll every granule from the start, 0 one granule first (default)
@@ -406,7 +414,8 @@ struct DecodeState {
 // dataflow layer counters (cnt, cnt_words u32; may be null).
 int step_start_launch(DecodeState* st, const int32_t* prompt, const unsigned long long* partials,
                       int n_partials, int32_t* tokens, const void* table, int table_dtype, int hidden,
-                      float* x, long long* xres, int max_seq, unsigned* cnt, int cnt_words, hipStream_t s);
+                      float* x, long long* xres, int max_seq, unsigned* cnt, int cnt_words, hipStream_t s,
+                      long long* xres2 = nullptr);  // xres2: a second copy of fixed(x) (layer 0's o_proj seed)
 // after the last forward: tokens[next_pos] = argmax(partials) (no state change)
 int finalize_launch(DecodeState* st, const unsigned long long* partials, int n_partials,
                     int32_t* tokens, int max_seq, hipStream_t s);

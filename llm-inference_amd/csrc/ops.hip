@@ -170,7 +170,7 @@ __global__ void argmax_final_kernel(const unsigned long long* partials, int np, 
 template <typename TT>
 __global__ void step_start_kernel(DecodeState* st, const int32_t* prompt, const unsigned long long* partials,
                                   int np, int32_t* tokens, const TT* table, int hidden, float* x,
-                                  long long* xres, int max_seq, unsigned* cnt, int cnt_words) {
+                                  long long* xres, int max_seq, unsigned* cnt, int cnt_words, long long* xres2) {
     __shared__ unsigned long long sh[16];
     for (int i = threadIdx.x; i < cnt_words; i += blockDim.x) cnt[i] = 0u;  // this token's layer counters
     __shared__ int tok_s;
@@ -211,6 +211,7 @@ __global__ void step_start_kernel(DecodeState* st, const int32_t* prompt, const 
         const float v = to_f32(row[i]);
         x[i] = v;
         if (xres) xres[i] = to_fixed(v);
+        if (xres2) xres2[i] = to_fixed(v);  // layer 0's o_proj sum starts from the residual too
     }
 }
 
@@ -483,13 +484,13 @@ int argmax_launch(const float* logits, int n, int32_t* out_id, unsigned long lon
 
 int step_start_launch(DecodeState* st, const int32_t* prompt, const unsigned long long* partials, int np,
                       int32_t* tokens, const void* table, int t_dtype, int hidden, float* x, long long* xres,
-                      int max_seq, unsigned* cnt, int cnt_words, hipStream_t s) {
+                      int max_seq, unsigned* cnt, int cnt_words, hipStream_t s, long long* xres2) {
     if (t_dtype == LLMI_F16)
         hipLaunchKernelGGL(step_start_kernel<__half>, dim3(1), dim3(1024), 0, s, st, prompt, partials, np, tokens,
-                           (const __half*)table, hidden, x, xres, max_seq, cnt, cnt ? cnt_words : 0);
+                           (const __half*)table, hidden, x, xres, max_seq, cnt, cnt ? cnt_words : 0, xres2);
     else
         hipLaunchKernelGGL(step_start_kernel<float>, dim3(1), dim3(1024), 0, s, st, prompt, partials, np, tokens,
-                           (const float*)table, hidden, x, xres, max_seq, cnt, cnt ? cnt_words : 0);
+                           (const float*)table, hidden, x, xres, max_seq, cnt, cnt ? cnt_words : 0, xres2);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }

@@ -37,10 +37,23 @@ int qa_grid_cap = 0;  // A/B: cap on the GEMV part of the grid (0 = every reside
 int qa_order = 1;     // 1: GEMV rows and attention blocks head-major (MHA); 0: natural order (A/B)
 int qa_poll_all = 0;  // 1: attention polls every granule from the start (A/B)
 
-template <typename WT, typename GT, int XPT, int U, typename KT>
-__global__ __launch_bounds__(256, (qa_minw<WT, U>())) void qkv_attn_kernel(GemvArgs g, AttnArgs at, int g_grid, int ns) {
+// WITH_O: blocks past the attention's run the o_proj (oproj_body2, FUSED: two heads per block,
+// W_o slices issued at once, then a wait on the pair's arrival counters), pair-major so the
+// heads the GEMV finishes first are projected first
+template <typename WT, typename GT, int XPT, int U, typename KT, bool WITH_O>
+__global__ __launch_bounds__(256, (qa_minw<WT, U>())) void qkv_attn_kernel(GemvArgs g, AttnArgs at, OprojArgs o,
+                                                                            int g_grid, int ns) {
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
     WgStamp ts(g.stamps);
+    if constexpr (WITH_O) {
+        const int ob = (int)blockIdx.x - g_grid - at.heads * at.nact;
+        if (ob >= 0) {
+            const int n_chunks = (o.n_rows + 63) / 64;
+            attn_detail::oproj_body2<WT, 8, PlainIO, true>(o, ob / n_chunks, ob % n_chunks, ns,
+                                                           reinterpret_cast<float*>(xs));
+            return;
+        }
+    }
     if ((int)blockIdx.x < g_grid) {
         gemv_detail::gemv_body<WT, gemv_detail::kRows, EPI_STORE, true, GT, XPT, U, true, PlainIO, 1, true>(
             g, blockIdx.x, g_grid, xs);
@@ -54,10 +67,11 @@ __global__ __launch_bounds__(256, (qa_minw<WT, U>())) void qkv_attn_kernel(GemvA
     }
 }
 
-template <typename WT, typename GT, int XPT, int U, typename KT>
-int launch_k(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
-    auto kern = qkv_attn_kernel<WT, GT, XPT, U, KT>;
-    const size_t lds = std::max(gemv_detail::gemv_lds_bytes(g.k), attn_detail::kAttnLds);
+template <typename WT, typename GT, int XPT, int U, typename KT, bool WITH_O>
+int launch_k(const GemvArgs& g, const AttnArgs& at, const OprojArgs* o, hipStream_t s) {
+    auto kern = qkv_attn_kernel<WT, GT, XPT, U, KT, WITH_O>;
+    size_t lds = std::max(gemv_detail::gemv_lds_bytes(g.k), attn_detail::kAttnLds);
+    if (WITH_O) lds = std::max(lds, attn_detail::oproj2_lds<8>());
     int G = gemv_grid(g);
     // resident blocks of this kernel: the GEMV takes at most all of them (a looping grid), the
     // attention blocks fill the slots GEMV blocks leave
@@ -73,26 +87,37 @@ int launch_k(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
     if (occ_blocks > 0 && G > occ_blocks) G = occ_blocks;
     if (qa_grid_cap > 0 && qa_grid_cap < G) G = qa_grid_cap;
     const int ns = (at.max_seq + attn_detail::CH - 1) / attn_detail::CH;
-    const int grid = G + at.heads * at.nact;
+    int grid = G + at.heads * at.nact;
     GemvArgs gg = g;
     AttnArgs aa = at;
+    OprojArgs oo;
     gg.tag_heads = (qa_order && at.heads == at.kv_heads && g.n_rows == 3 * at.heads * attn_detail::D) ? at.heads : 0;
     aa.tag_poll_all = qa_poll_all;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, gg, aa, G, ns);
+    if (WITH_O) {
+        oo = *o;
+        aa.publish = 1;
+        grid += (at.heads / 2) * ((o->n_rows + 63) / 64);
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, gg, aa, oo, G, ns);
     LLMI_HIP(hipGetLastError());
     return LLMI_OK;
 }
 
 template <typename WT, typename GT, int XPT, int U>
-int launch_kt(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
-    return at.cache_dtype == LLMI_F16 ? launch_k<WT, GT, XPT, U, __half>(g, at, s)
-                                      : launch_k<WT, GT, XPT, U, float>(g, at, s);
+int launch_kt(const GemvArgs& g, const AttnArgs& at, const OprojArgs* o, hipStream_t s) {
+    if constexpr (sizeof(WT) == 2 && XPT == 4 && U == 4) {  // the o_proj part: fp16 7B-width shapes
+        if (o)
+            return at.cache_dtype == LLMI_F16 ? launch_k<WT, GT, XPT, U, __half, true>(g, at, o, s)
+                                              : launch_k<WT, GT, XPT, U, float, true>(g, at, o, s);
+    }
+    return at.cache_dtype == LLMI_F16 ? launch_k<WT, GT, XPT, U, __half, false>(g, at, nullptr, s)
+                                      : launch_k<WT, GT, XPT, U, float, false>(g, at, nullptr, s);
 }
 
 template <typename WT, typename GT>
-int launch_w(const GemvArgs& g, const AttnArgs& at, int xpt, int u, hipStream_t s) {
-    if (xpt == 4) return u == 4 ? launch_kt<WT, GT, 4, 4>(g, at, s) : launch_kt<WT, GT, 4, 5>(g, at, s);
-    return u == 4 ? launch_kt<WT, GT, 5, 4>(g, at, s) : launch_kt<WT, GT, 5, 5>(g, at, s);
+int launch_w(const GemvArgs& g, const AttnArgs& at, const OprojArgs* o, int xpt, int u, hipStream_t s) {
+    if (xpt == 4) return u == 4 ? launch_kt<WT, GT, 4, 4>(g, at, o, s) : launch_kt<WT, GT, 4, 5>(g, at, o, s);
+    return u == 4 ? launch_kt<WT, GT, 5, 4>(g, at, o, s) : launch_kt<WT, GT, 5, 5>(g, at, o, s);
 }
 
 
@@ -136,7 +161,18 @@ void qkv_attn_set_grid(int cap) { qa_grid_cap = cap > 0 ? cap : 0; }
 void qkv_attn_set_order(int head_major) { qa_order = head_major != 0; }
 void qkv_attn_set_poll(int all) { qa_poll_all = all != 0; }
 
-int qkv_attn_launch(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
+bool qkv_attn_o_supported(const GemvArgs& g, const AttnArgs& at, const OprojArgs& o) {
+    if (!qkv_attn_supported(g, at) || g.w_dtype != LLMI_F16 || g.k / 4 > 4 * 256 || pick_u(g) != 4) return false;
+    if (at.xacc != nullptr || at.heads % 2 != 0 || at.heads != at.kv_heads) return false;
+    return o.w_dtype == LLMI_F16 && !o.head_major && o.heads == at.heads && o.nact == at.nact && o.xacc &&
+           o.workspace == at.workspace && o.n_rows % 64 == 0 && o.ldw >= o.heads * attn_detail::D &&
+           (long)o.heads * o.n_rows / (1024 * 16) >= 8 && !o.xt.buf;  // oproj_npl 8, no fused exchange
+}
+
+int qkv_attn_launch(const GemvArgs& g, const AttnArgs& at, hipStream_t s) { return qkv_attn_o_launch(g, at, nullptr, s); }
+
+int qkv_attn_o_launch(const GemvArgs& g, const AttnArgs& at, const OprojArgs* o, hipStream_t s) {
+    LLMI_REQUIRE(!o || qkv_attn_o_supported(g, at, *o), "qkv_attn_o: unsupported shape (qkv_attn_o_supported)");
     LLMI_REQUIRE(qkv_attn_supported(g, at), "qkv_attn: unsupported shape (qkv_attn_supported)");
     LLMI_REQUIRE(g.w && g.x_fixed && g.y_tag && g.tag_epoch && at.qkv_tag == g.y_tag && at.tag_epoch == g.tag_epoch &&
                      at.tag_layer == g.tag_layer && g.tag_layer < 128,
@@ -148,9 +184,9 @@ int qkv_attn_launch(const GemvArgs& g, const AttnArgs& at, hipStream_t s) {
     const int xpt = g.k / 4 <= 4 * 256 ? 4 : 5;
     const int u = pick_u(g);
     switch (g.w_dtype) {
-        case LLMI_F16: return launch_w<__half, __half>(g, at, xpt, u, s);
-        case LLMI_F32: return launch_w<float, float>(g, at, xpt, u, s);
-        case LLMI_I8: return launch_w<int8_t, __half>(g, at, xpt, u, s);
+        case LLMI_F16: return launch_w<__half, __half>(g, at, o, xpt, u, s);
+        case LLMI_F32: return launch_w<float, float>(g, at, nullptr, xpt, u, s);
+        case LLMI_I8: return launch_w<int8_t, __half>(g, at, nullptr, xpt, u, s);
     }
     return LLMI_EINVAL;
 }

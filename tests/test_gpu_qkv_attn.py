@@ -38,18 +38,21 @@ def test_fused_equals_two_launches(case):
     cfg.weight_dtype, cfg.kv_dtype = wdt, kv
     prompt = synth_prompt(3, 8, cfg.vocab)
     out = {}
+    variants = {0: (0, 0), 1: (1, 0), 2: (1, 1)}  # separate launches / fused q/k/v + attention / + o_proj
     with Engine(cfg) as e:
         e.load_synthetic(7)
-        for v in (0, 1):
-            e.set_option("qkv_attn", v)
+        for v, (qa, qo) in variants.items():
+            e.set_option("qkv_attn", qa)
+            e.set_option("qa_o", qo)
             for g in (True, False):
                 n = 150 if g else 70  # graph: ctx 158, three split counts
                 toks = e.generate(prompt, n, use_graph=g)
                 out[(v, g)] = (toks.copy(), e.logits().copy(), e.hidden().copy())
-    for g in (True, False):
-        for i in range(3):
-            np.testing.assert_array_equal(out[(1, g)][i], out[(0, g)][i])
-    print(f"{case}: fused q/k/v + attention bitwise equal to the two launches (graph and eager)")
+    for v in (1, 2):
+        for g in (True, False):
+            for i in range(3):
+                np.testing.assert_array_equal(out[(v, g)][i], out[(0, g)][i])
+    print(f"{case}: fused q/k/v + attention (+ o_proj) bitwise equal to the separate launches (graph and eager)")
 
 
 def test_fused_reference_fixtures():
@@ -60,6 +63,7 @@ def test_fused_reference_fixtures():
     cfg.kv_dtype = _lib.F32
     with Engine(cfg) as e:
         e.set_option("qkv_attn", 1)
+        e.set_option("qa_o", 1)
         e.load_synthetic(int(f["seed"]))
         toks = e.generate(f["prompt"], len(f["tokens"]))
         np.testing.assert_array_equal(toks, f["tokens"])
@@ -71,6 +75,7 @@ def test_fused_reference_fixtures():
     cfg.kv_dtype = _lib.F16
     with Engine(cfg) as e:
         e.set_option("qkv_attn", 1)
+        e.set_option("qa_o", 1)
         e.load_synthetic(int(f["seed"]))
         toks = e.generate(f["prompt"], len(f["tokens"]))
         np.testing.assert_array_equal(toks, f["f16kv_tokens"])
@@ -90,6 +95,7 @@ def test_fused_one_layer_across_prompts():
         e.load_synthetic(5)
         for v in (0, 1):
             e.set_option("qkv_attn", v)
+            e.set_option("qa_o", v)
             res[v] = []
             for p in ([3], [11], [3], [29, 4]):
                 t = e.generate(np.array(p, np.int32), 1)
@@ -107,6 +113,7 @@ def test_fused_position_mismatch_is_reported(use_graph):
     prompt = synth_prompt(1, 8, cfg.vocab)
     with Engine(cfg) as e:
         e.set_option("qkv_attn", 1)
+        e.set_option("qa_o", 1)
         e.load_synthetic(2)
         e.set_prompt(prompt)
         e.decode(len(prompt), use_graph=use_graph)
