@@ -542,6 +542,10 @@ def main():
     # dominant kernel: gate_up GEMV, timed with HIP events on the engine stream
     gu_us, gu_bytes = eng.time_kernel("gate_up", iters=256)
     kern = {k: eng.time_kernel(k, iters=128) for k in ("qkv", "attn", "o", "down", "lm_head")}
+    try:  # the decode graph's q/k/v + attention launch (the two kernels above, fused)
+        kern["qkv_attn"] = eng.time_kernel("qkv_attn", iters=128)
+    except Exception as e:  # reported, never fatal to the GPU number
+        progress(f"qkv_attn timing skipped: {e!r}"[:200])
     try:
         peak_meas = hbm_read_peak(gu_bytes)
     except Exception as e:  # reported, never fatal to the GPU number

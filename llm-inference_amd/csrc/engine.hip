@@ -1818,8 +1818,18 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
                 return llmi::xchg_launch(g.xchg_args(g.xacc, (int)H, 0, 3), g.stream);
             case 10:  // the persistent ring layer (o_proj, gate_up, down, next q/k/v)
                 return llmi::ring_layer_launch(g.ring_args(l, true), g.n_cu, g.stream);
+            case 11: {  // the fused q/k/v + attention launch (the decode default; consecutive launches
+                        // cycle layers, so each finds the previous layer's tags in the granule buffer)
+                llmi::GemvArgs q = g.qkv_args(l);
+                llmi::AttnArgs at = g.attn_args(l);
+                q.kpar = 0;
+                q.y_tag = g.qtag; q.tag_epoch = &g.st->epoch; q.tag_layer = (unsigned)l;
+                at.qkv_tag = g.qtag; at.tag_epoch = &g.st->epoch; at.tag_layer = (unsigned)l;
+                at.xacc = nullptr;  // (timing only: no residual seed)
+                return llmi::qkv_attn_launch(q, at, g.stream);
+            }
         }
-        LLMI_REQUIRE(false, "time_kernel: which must be 0..10");
+        LLMI_REQUIRE(false, "time_kernel: which must be 0..11");
     };
     LLMI_REQUIRE(which < 6 || which > 7 || g.comm != nullptr,
                  "time_kernel: the all-reduce needs an RCCL communicator (tp_id)");
@@ -1844,6 +1854,14 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
         case 8:
         case 9: b = (uint64_t)H * 8; break;
         case 10: b = ((uint64_t)H * g.ql + 3ull * g.il * H + (uint64_t)(g.ql + 2 * g.kvrows) * H) * ws; break;
+        case 11: {
+            llmi::DecodeState hs;
+            LLMI_HIP(hipMemcpy(&hs, g.st, sizeof(hs), hipMemcpyDeviceToHost));
+            const uint64_t eb = llmi::dtype_size(g.c.kv_dtype);
+            b = (uint64_t)(g.ql + 2 * g.kvrows) * H * ws + (g.ql + 2 * g.kvrows) * sc +
+                (uint64_t)2 * (hs.cur_pos + 1) * g.kvl * g.c.head_dim * eb + 2ull * g.kvl * g.c.head_dim * eb;
+            break;
+        }
     }
     // timing launches modify the residual stream (o/down epilogues add into x),
     // so save and restore the small activation state around them
@@ -1861,7 +1879,9 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     auto kv_rows = [&](int l, int v) {
         return (char*)(v ? g.vcache : g.kcache) + (size_t)l * g.kv_layer_elems * kv_eb + (size_t)hst.cur_pos * kv_row;
     };
-    if (which == 1) {
+    LLMI_REQUIRE(which != 11 || (g.layers.size() >= 2 && g.c.layers < 128),
+                 "time_kernel: the fused q/k/v + attention launch cycles >= 2 layers (its tags must change)");
+    if (which == 1 || which == 11) {
         LLMI_HIP(hipMemcpyAsync(&hst, g.st, sizeof(hst), hipMemcpyDeviceToHost, g.stream));
         LLMI_HIP(hipStreamSynchronize(g.stream));
         save_kv.resize((size_t)g.c.layers * 2 * g.kvl * kv_row);
@@ -1904,7 +1924,7 @@ int llmi_engine_time_kernel(llmi_engine* e, int which, int iters, float* avg_us,
     if (cg) (void)hipGraphDestroy(cg);
     LLMI_HIP(hipMemcpy(g.x, save.data(), H * 4, hipMemcpyHostToDevice));
     for (int i = 0; i < 3; ++i) LLMI_HIP(hipMemcpy(fx[i], save_fx.data() + i * H * 8, H * 8, hipMemcpyHostToDevice));
-    if (which == 1)
+    if (which == 1 || which == 11)
         for (int l = 0; l < g.c.layers; ++l)
             for (int v = 0; v < 2; ++v)
                 LLMI_HIP(hipMemcpy2D(kv_rows(l, v), kv_pitch, save_kv.data() + ((size_t)l * 2 + v) * g.kvl * kv_row,

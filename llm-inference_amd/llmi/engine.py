@@ -135,7 +135,7 @@ class Engine:
     # allreduce / allreduce_graph: one residual all-reduce of the TP exchange (needs a tp_id),
     # launched eagerly / replayed from a captured graph of `iters` calls
     KERNELS = {"qkv": 0, "attn": 1, "o": 2, "gate_up": 3, "down": 4, "lm_head": 5, "allreduce": 6,
-               "allreduce_graph": 7, "xchg": 8, "xchg_graph": 9, "ring": 10}
+               "allreduce_graph": 7, "xchg": 8, "xchg_graph": 9, "ring": 10, "qkv_attn": 11}
 
     # one-shot peer exchange (tensor parallel without RCCL in the token graph)
     def xchg_handle(self) -> bytes:

@@ -53,9 +53,9 @@ for s in "$@"; do
       for c in FETCH_SIZE WRITE_SIZE; do
         step "pmc $c"
         rm -rf /tmp/pmc_$c
-        timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex 'gemv_kernel|attn_decode_kernel|attn_oproj2?_kernel' \
+        timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex 'gemv_kernel|attn_decode_kernel|attn_oproj2?_kernel|qkv_attn_kernel' \
           -d /tmp/pmc_$c -o pmc --output-format csv -- python3 tools/kernel_probe.py --ctx 2048 --prefill --iters 8 \
-          --kernels gate_up,qkv,lm_head,attn,o,down > $OUT/pmc_${c}_$TAG.log 2>&1 || fail $? pmc $OUT/pmc_${c}_$TAG.log
+          --kernels gate_up,qkv,lm_head,attn,o,down,qkv_attn > $OUT/pmc_${c}_$TAG.log 2>&1 || fail $? pmc $OUT/pmc_${c}_$TAG.log
         find /tmp/pmc_$c -name '*counter_collection.csv' -exec cp {} $OUT/pmc_${c}_$TAG.csv \;
       done ;;
     pftrace)
