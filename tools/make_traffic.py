@@ -15,7 +15,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # attention at ctx 2048 (kernel_probe --ctx 2048): 2 * 2048 * 32 * 128 * 2 B of K/V + the new slot
 ALG = {"qkv": 100663296, "gate_up": 180355072, "down": 90177536, "lm_head": 262144000, "attn": 33570816,
-       "o": 33554432,
+       "o": 33554432, "qkv_attn": 100663296 + 33570816,
        # config 5 (tools/int8_probe.py, Llama-2-13B shape): int8 weights + fp16 row scales
        "i8_qkv": 15360 * 5120 + 15360 * 2, "i8_o": 5120 * 5120 + 5120 * 2,
        "i8_gate_up": 27648 * 5120 + 27648 * 2, "i8_down": 5120 * 13824 + 5120 * 2}
@@ -39,6 +39,8 @@ def role(name):
         return "attn"
     if "attn_oproj_kernel<__half" in name or "attn_oproj2_kernel<__half" in name:
         return "o"
+    if "qkv_attn_kernel<__half, __half, 4, 4, __half, false>" in name:
+        return "qkv_attn"
     return None
 
 
