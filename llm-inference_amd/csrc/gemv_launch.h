@@ -17,12 +17,18 @@ namespace gemv_detail {
 #endif
 
 #ifndef LLMI_GEMV_MIN_WAVES_I8
-#define LLMI_GEMV_MIN_WAVES_I8 LLMI_GEMV_MIN_WAVES  // int8: 16 weights per load need 4 float4 of x each
+// int8 at unroll <= 5: 4 waves per SIMD. The 13B-width q/k/v / gate_up / lm_head kernels need 130-135
+// VGPRs (3 waves) for a prologue peak (the 5 x 16-B x-staging loads with gammas beside the first
+// weight batch); capped at 128 they spill 2-4 VGPRs there and run 0.5 % faster a 13B token (same
+// box, alternating libraries: 3,133 -> 3,115 us, profiles/r07i_int8_minwaves_ab.jsonl)
+#define LLMI_GEMV_MIN_WAVES_I8 4
 #endif
-template <typename WT> constexpr int min_waves() { return sizeof(WT) == 1 ? LLMI_GEMV_MIN_WAVES_I8 : LLMI_GEMV_MIN_WAVES; }
+template <typename WT, int U> constexpr int min_waves() {
+    return sizeof(WT) == 1 && U <= 5 ? LLMI_GEMV_MIN_WAVES_I8 : LLMI_GEMV_MIN_WAVES;
+}
 
 template <typename WT, int ROWS, int EPI, bool NORM, typename GT, int XPT, int kUnroll, bool XFIX, int KPT = 1>
-__global__ __launch_bounds__(kThreads, min_waves<WT>()) void gemv_kernel(GemvArgs a) {
+__global__ __launch_bounds__(kThreads, (min_waves<WT, kUnroll>())) void gemv_kernel(GemvArgs a) {
     // all LDS in one 16-B aligned dynamic region (cdna_hip_programming.md G17):
     // [PK][nc] float4 x image, then 16 floats of reduction scratch, then keys
     extern __shared__ __attribute__((aligned(16))) float4 xs[];
