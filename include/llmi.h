@@ -507,7 +507,12 @@ int llmi_engine_xchg_loopback(llmi_engine* e);
 /* Engine tuning switches for same-process A/B (no reference counterpart); the captured
  * token graphs are rebuilt on the next decode. "kpar": 1 (default) lets a TP rank's q/k/v and
  * gate_up GEMVs split K over 2 or 4 waves of a workgroup when one row group per wave would
- * leave CUs idle or doubled (tp_world > 1 only), 0 keeps one wave per row group. */
+ * leave CUs idle or doubled (tp_world > 1 only), 0 keeps one wave per row group.
+ * "qkv_attn": 1 (default) runs a layer's q/k/v GEMV and split-KV attention as one launch (q/k/v
+ * handed over as tagged 8-byte granules; bitwise the two launches), 0 as two. "qa_o": 1 adds the
+ * o_proj to that launch (fp16 MHA, single rank; default 0, measured slower). "qa_grid" (workgroups
+ * of the fused launch's GEMV part, 0 = every resident slot), "qa_order" (1 head-major rows and
+ * attention blocks, default), "qa_poll" (1 poll every granule from the start): A/B only. */
 int llmi_engine_set_option(llmi_engine* e, const char* name, int value);
 int llmi_engine_set_exchange(llmi_engine* e, int mode);
 /* Diagnostics: kernels launched by llmi_engine_time_kernel (and graphs built
