@@ -1197,8 +1197,16 @@ struct Engine {
         int so = (ql % (kPfSplit * 64)) == 0 ? kPfSplit : 1;
         g.lda = ql; g.w = L.o; g.w_kblock = 0; g.n = H; g.k = ql;
         g.epi = EPI_SLAB; g.ksplit = so; g.slab = pf_slab; g.y = pf_x; g.ldy = H;
+        static const bool o3 = [] {  // A/B: LLMI_PF_O3=1 puts the fp16 o_proj on gemm3 (8 K slices) too; measured
+                                     // 0.1 ms slower a 7B prefill than gemm2's 2 slices (r07l), so gemm2 stays
+            const char* e = std::getenv("LLMI_PF_O3");
+            return e && std::string(e) == "1";
+        }();
         if (f8) {
             so = kPfDown; g.ksplit = so; g.w8 = W8->o; g.w8_exp = W8->o_e;
+            LLMI_TRY(gemm3_launch(g, stream));
+        } else if (o3 && gemm3_supported(H, ql, EPI_SLAB, kPfDown)) {
+            so = kPfDown; g.ksplit = so;
             LLMI_TRY(gemm3_launch(g, stream));
         } else {
             LLMI_TRY(gemm2_launch(g, stream));

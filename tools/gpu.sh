@@ -9,6 +9,7 @@
 #   pmc               FETCH_SIZE and WRITE_SIZE passes (separate runs) on the decode kernels
 #   pftrace           rocprofv3 kernel trace of a 512-row prefill (PF_MODE env: exact | exact8 | fast, default exact8)
 #   mfma              MFMA-busy PMC pass on the prefill GEMMs / attention
+#   lds               LDS bank-conflict / LDS-instruction PMC pass on the prefill GEMMs / attention
 #   cmd=<command>     any other command, under a 600-s limit, output in gpurun_out/cmd_<tag>_<n>.log
 # Every output lands in gpurun_out/<step>_<tag>.*; copy what is judged into profiles/.
 set -o pipefail
@@ -71,6 +72,13 @@ for s in "$@"; do
         --kernel-include-regex 'gemm[23]?_(sk_)?kernel|attn_prefill' -d /tmp/pmc_m -o pmc --output-format csv -- \
         python3 tools/prefill_probe.py 512 3 ${PF_MODE:-exact} > $OUT/mfma_$TAG.log 2>&1 || fail $? mfma $OUT/mfma_$TAG.log
       find /tmp/pmc_m -name '*counter_collection.csv' -exec cp {} $OUT/pmc_mfma_$TAG.csv \; ;;
+    lds)
+      step "pmc lds (prefill GEMMs / attention)"
+      rm -rf /tmp/pmc_l
+      timeout -k 10 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE \
+        --kernel-include-regex 'gemm[23]?_(sk_)?kernel|attn_prefill' -d /tmp/pmc_l -o pmc --output-format csv -- \
+        python3 tools/prefill_probe.py 512 3 ${PF_MODE:-exact} > $OUT/lds_$TAG.log 2>&1 || fail $? lds $OUT/lds_$TAG.log
+      find /tmp/pmc_l -name '*counter_collection.csv' -exec cp {} $OUT/pmc_lds_$TAG.csv \; ;;
     cmd=*)
       c=${s#cmd=}
       step "$c"
