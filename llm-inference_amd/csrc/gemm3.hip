@@ -614,6 +614,12 @@ __global__ __launch_bounds__(kT) void gemm3_silu_bal_kernel(Gemm2Args a) {
 // finish (a count in sk_ctl[32]) stores E there, so eager launches and graph replays alike
 // see a new value each launch. Every workgroup is resident (sk_grid <= the CU count, one
 // 136-KB workgroup per CU), so waits end unless another stream or process holds CUs.
+// Concurrency contract: sk_ctl / sk_flags / the slots belong to ONE
+// (device, stream) workspace and assume its launches never overlap -- a graph captured on
+// stream S must be replayed on S (or with S idle), never beside eager stream-K work on S's
+// workspace: two overlapping launches would share the ctl[32] count and the epoch and could
+// pass each other's flags silently. The engine and the layer API keep one workspace per
+// stream and replay their graphs on the stream they captured them on.
 #ifndef LLMI_SK_EXP
 #define LLMI_SK_EXP 0  // timing-only builds: 1 = flags without the slot payload, 2 = no hand-off at all
 #endif
