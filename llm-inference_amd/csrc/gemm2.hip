@@ -19,8 +19,8 @@
 // BK = 64, operands staged global -> LDS by global_load_lds_dwordx4 (no VGPRs,
 // no ds_write pass) into two LDS stages: stage k+1 is in flight while stage k is
 // multiplied. The LDS image is lane-linear (the DMA writes wave base + 16 * lane)
-// with the st_16x32 XOR swizzle (byte bit 5 ^= bit 9) applied on the global
-// SOURCE address, so the fragment ds_read_b128s spread over the banks. Workgroup
+// with an XOR swizzle (swz below) applied on the global SOURCE address, so the fragment
+// ds_read_b128s spread over the banks. Workgroup
 // ids are remapped (bijectively) so consecutive tiles share an XCD.
 // Roofline: MFMA (fp16 dense 2.5 PFLOP/s); FLOPs per launch 2 * M * N * K
 // (P = 2 issues 2x that on the matrix cores).
@@ -56,7 +56,18 @@ constexpr int kRowB = kBK * 2;  // 128-B LDS rows
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) const void* glb_ptr_t;
 
-__device__ __forceinline__ int swz(int b) { return b ^ (((b >> 9) & 1) << 5); }
+// LDS image swizzle (an involution on 2-KB blocks): 16-B chunk c of 128-B row r is stored at
+// chunk c ^ ((r >> 1) & 7) -- gemm3's swz3, under which the 16 lanes of each fragment
+// ds_read_b128 lane group hit 16 distinct 16-B bank slots. (The st_16x32 XOR, byte bit 5 ^=
+// bit 9, that this kernel used before left them 2-way conflicted: 4 bank-conflict cycles per
+// LDS instruction on the prefill o_proj, profiles/r07k_prefill_lds_pmc.json.) LLMI_GEMM2_SWZ=0:
+// the old XOR (A/B builds).
+#ifndef LLMI_GEMM2_SWZ
+#define LLMI_GEMM2_SWZ 1
+#endif
+__device__ __forceinline__ int swz(int b) {
+    return LLMI_GEMM2_SWZ ? b ^ (((b >> 8) & 7) << 4) : b ^ (((b >> 9) & 1) << 5);
+}
 
 #ifndef LLMI_GEMM2_STAGES
 #define LLMI_GEMM2_STAGES 3
