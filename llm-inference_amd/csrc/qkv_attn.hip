@@ -33,9 +33,11 @@ template <typename WT, int U> constexpr int qa_minw() { return (sizeof(WT) >= 2 
 namespace llmi {
 namespace {
 
-int qa_grid_cap = 0;  // A/B: cap on the GEMV part of the grid (0 = every resident slot); qkv_attn_set_grid
-int qa_order = 1;     // 1: GEMV rows and attention blocks head-major (MHA); 0: natural order (A/B)
-int qa_poll_all = 0;  // 1: attention polls every granule from the start (A/B)
+// A/B switches (engine options qa_grid / qa_order / qa_poll): process-wide, read at launch (graph
+// capture) time, so an engine's already captured graphs keep the values they were captured with
+int qa_grid_cap = 0;  // cap on the GEMV part of the grid (0 = every resident slot); qkv_attn_set_grid
+int qa_order = 1;     // 1: GEMV rows and attention blocks head-major (MHA); 0: natural order
+int qa_poll_all = 0;  // 1: attention polls every granule from the start
 
 // WITH_O: blocks past the attention's run the o_proj (oproj_body2, FUSED: two heads per block,
 // W_o slices issued at once, then a wait on the pair's arrival counters), pair-major so the
