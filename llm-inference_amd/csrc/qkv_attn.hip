@@ -28,7 +28,12 @@
 // waves per SIMD the kernel is built for (= workgroups per CU): 4, as the q/k/v GEMV alone, where
 // that fits 128 VGPRs without spills (fp16 / fp32 weights at U = 4: 125 / 110), else 3 (int8 and
 // U = 5 spilled 6-11 VGPRs at 4)
-template <typename WT, int U> constexpr int qa_minw() { return (sizeof(WT) >= 2 && U == 4) || sizeof(WT) == 4 ? 4 : 3; }
+#ifndef LLMI_QA_MINW_SPILL
+#define LLMI_QA_MINW_SPILL 3  // waves per SIMD for the shapes that spill at 4 (A/B builds: 4)
+#endif
+template <typename WT, int U> constexpr int qa_minw() {
+    return (sizeof(WT) >= 2 && U == 4) || sizeof(WT) == 4 ? 4 : LLMI_QA_MINW_SPILL;
+}
 
 namespace llmi {
 namespace {
