@@ -28,6 +28,7 @@ CASES = {
     "7b_f16_f32kv": ("llama2-7b", _lib.F16, _lib.F32),
     "13b_i8_f16kv": ("llama2-13b", _lib.I8, _lib.F16),
     "tiny_f32_f32kv": ("tiny", _lib.F32, _lib.F32),
+    "tiny_gqa_f16kv": ("tiny", _lib.F16, _lib.F16),  # kv_heads = heads / 2: natural row order
 }
 
 
@@ -36,6 +37,8 @@ def test_fused_equals_two_launches(case):
     pname, wdt, kv = CASES[case]
     cfg = preset(pname, layers=2, max_seq=200)
     cfg.weight_dtype, cfg.kv_dtype = wdt, kv
+    if "gqa" in case:
+        cfg.kv_heads = cfg.heads // 2
     prompt = synth_prompt(3, 8, cfg.vocab)
     out = {}
     variants = {0: (0, 0), 1: (1, 0), 2: (1, 1)}  # separate launches / fused q/k/v + attention / + o_proj
