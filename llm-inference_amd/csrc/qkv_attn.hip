@@ -158,6 +158,21 @@ bool qkv_attn_supported(const GemvArgs& g, const AttnArgs& at) {
     if (g.w_dtype == LLMI_I8 && !g.scales) return false;
     const int u = pick_u(g);
     if (u != 4 && u != 5) return false;
+    // where the standalone GEMV would stream a row group in one unroll-8 batch and its grid fills
+    // every CU at least twice (a TP-2 rank's q/k/v: 768 workgroups), the fused form's unroll 4
+    // costs more than the boundary it saves (TP 2 1,961 -> 1,982 us a token, r07s); with fewer
+    // workgroups than that (TP 4: 384, TP 8: 192) it wins (-1.8 % / -4.1 %, r07e)
+    {
+        const int groups = (g.n_rows + gemv_detail::kRows - 1) / gemv_detail::kRows;
+        int su = 0;
+        switch (g.w_dtype) {
+            case LLMI_F16: su = gemv_detail::pick_unroll<__half, EPI_STORE>(g, groups); break;
+            case LLMI_F32: su = gemv_detail::pick_unroll<float, EPI_STORE>(g, groups); break;
+            case LLMI_I8: su = gemv_detail::pick_unroll<int8_t, EPI_STORE>(g, groups); break;
+        }
+        const int cus = gemv_detail::device_cus() > 0 ? gemv_detail::device_cus() : 256;
+        if (su != u && gemv_grid(g) >= 2 * cus) return false;
+    }
     if (at.head_dim != attn_detail::D || at.nact <= 0 || !at.pos_dev || at.direct_out) return false;
     if (at.cache_dtype != LLMI_F16 && at.cache_dtype != LLMI_F32) return false;
     if (at.heads <= 0 || at.kv_heads <= 0 || at.heads % at.kv_heads != 0) return false;
